@@ -1,0 +1,109 @@
+/*
+ * psgd_oracle.h -- CPU restatement of the reference's parallelized-SGD hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY. Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library; the product path never does.
+ *
+ * Parity status: PARTIALLY PINNED. The reference (Scala 2.10/2.11 on Spark 1.6.1) cannot be
+ * built or run here (no JVM, no jars, no network). The restatement is pinned against the
+ * reference suite's own known-answer properties (ParallelizedSGDSuite.scala:101, :132-141, :180)
+ * and cross-checked bit-for-bit against an independent pure-Python restatement
+ * (oracle/psgd_ref.py). Absolute weight/loss values are otherwise unpinned.
+ *
+ * Semantics restated (all file:line are into /root/reference):
+ *   driver loop            ParallelizedSGD.scala:188-306
+ *   chain (mapPartitions)  ParallelizedSGD.scala:243-270
+ *   combine (treeReduce)   ParallelizedSGD.scala:271-276
+ *   isConverged            ParallelizedSGD.scala:324-336
+ *   updaters               SGDUpdater.scala:86-98 (Simple), :126-148 (L1), :163-181 (SquaredL2),
+ *                          :199-227 (AdaGrad), :252-285 (Adam)
+ *   gradients              [ext] Spark MLlib 1.6.1 mllib/optimization/Gradient.scala
+ *                          (LogisticGradient binary, LeastSquaresGradient, HingeGradient),
+ *                          with BLAS.dot/axpy/scal on netlib-java F2J ddot/daxpy/dscal
+ *                          (sequential left folds, no fused multiply-add) and
+ *                          MLUtils.log1pExp.
+ */
+#ifndef PSGD_ORACLE_H
+#define PSGD_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { OR_GRAD_LOGISTIC = 0, OR_GRAD_LEAST_SQUARES = 1, OR_GRAD_HINGE = 2 };
+enum { OR_UPD_SIMPLE = 0, OR_UPD_SQUARED_L2 = 1, OR_UPD_L1 = 2, OR_UPD_ADAGRAD = 3, OR_UPD_ADAM = 4 };
+
+/* Combine order for the per-partition results (ParallelizedSGD.scala:271-276).
+ * group_offsets (nullable) splits the chains into contiguous groups: each group is
+ * left-folded in chain order, then the group results are left-folded in group order
+ * (a two-level tree, the order the multi-GPU build uses: chains within a GPU, then GPUs). */
+
+/* One partition = rows [row_begin, row_end) of a global matrix, in iterator order.
+ * Dense: X is row-major with leading dimension ld (>= d).
+ * CSR:   row_ptr[N+1] (global), col/val indexed by row_ptr; indices strictly increasing. */
+typedef struct {
+    int64_t n_total;       /* N rows in the global matrix */
+    int32_t d;
+    int32_t is_csr;
+    const double* labels;  /* [N] */
+    const double* X;       /* dense [N*ld] */
+    int64_t ld;
+    const int64_t* row_ptr;
+    const int32_t* col;
+    const double* val;
+} or_matrix;
+
+typedef struct {
+    int32_t gradient;
+    int32_t updater;
+    double step_size;
+    double reg_param;
+    double convergence_tol;
+    double adam_beta, adam_gamma, adam_eps;
+} or_params;
+
+/* One chain (ParallelizedSGD.scala:243-270) over rows [r0, r1). */
+int or_chain(const or_matrix* m, int64_t r0, int64_t r1, const or_params* prm,
+             const double* w_in, double* w_out, double* rv_out, double* loss_out,
+             int64_t* count_out);
+
+/* Reference pairwise combine (ParallelizedSGD.scala:271-276), in place into acc. */
+void or_combine(int32_t d, double* acc_w, double* acc_rv, double* acc_loss, int64_t* acc_c,
+                const double* w2, double rv2, double loss2, int64_t c2);
+
+/* isConverged (ParallelizedSGD.scala:324-336). */
+int or_is_converged(int32_t d, const double* prev, const double* cur, double tol);
+
+/* Updater regVal at iteration 0 (ParallelizedSGD.scala:231-233). */
+double or_initial_regval(int32_t d, const double* w, const or_params* prm);
+
+/* Full driver (ParallelizedSGD.scala:188-306) with miniBatchFraction == 1.0.
+ * part_offsets[P+1]: partition p holds rows [part_offsets[p], part_offsets[p+1]).
+ * Returns number of loss-history entries in *n_hist (<= num_iterations).
+ * chain_counts (nullable): [num_iterations * P], per-iteration per-chain processed counts.
+ * n_threads: worker threads for the chains (results do not depend on it). */
+int or_run(const or_matrix* m, int32_t P, const int64_t* part_offsets,
+           const int32_t* group_offsets, int32_t n_groups,
+           const or_params* prm, int32_t num_iterations, const double* w0,
+           double* w_out, double* loss_hist, int32_t* n_hist, int64_t* chain_counts,
+           int32_t n_threads);
+
+/* One epoch of chains only (no combine): per-chain outputs, for the CPU baseline timer. */
+int or_run_chains(const or_matrix* m, int32_t P, const int64_t* part_offsets,
+                  const int64_t* part_limits, const or_params* prm, const double* w_in,
+                  double* w_out /*[P*d]*/, double* rv_out, double* loss_out, int64_t* count_out,
+                  int32_t n_threads);
+
+/* java.util.Random + StrictMath.log (fdlibm) restatements, for the suite's data generator
+ * (ParallelizedSGDSuite.scala:42-62). */
+double or_fdlibm_log(double x);
+void or_generate_gd_input(double offset, double scale, int32_t n, int32_t seed,
+                          double* x_out, double* y_out);
+void or_jrandom_doubles(int64_t seed, int32_t n, double* out);
+void or_jrandom_gaussians(int64_t seed, int32_t n, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
