@@ -1,0 +1,151 @@
+/*
+ * psgd.h -- C ABI of the MI355X-native parallelized-SGD hot path.
+ *
+ * This is the drop-in boundary for the reference's per-partition SGD loop. The host (a Scala
+ * shim over JNI/Panama, or the Python package in this repo over ctypes) keeps the driver loop of
+ * ParallelizedSGD.runParallelizedSGD (ParallelizedSGD.scala:188-306) and replaces the
+ * broadcast + mapPartitions + treeReduce block (ParallelizedSGD.scala:238-276) with one
+ * psgd_run_epoch call per process and iteration.
+ *
+ * All file:line citations are into the reference (Patrickgsheng/spark-parallelized-sgd):
+ *   PSGD = src/main/scala/org/apache/spark/mllib/optimization/ParallelizedSGD.scala
+ *   UPD  = src/main/scala/org/apache/spark/mllib/optimization/SGDUpdater.scala
+ *
+ * Conventions: plain C types only; 0 = success, negative = error (psgd_last_error() holds the
+ * thread-local message). PSGD_EINVAL maps to IllegalArgumentException on the JVM side (the
+ * reference's `require` failures), everything else to RuntimeException.
+ * Pointers named d_* are device pointers on the context's device; all others are host memory
+ * owned by the caller. `stream` arguments are hipStream_t passed as void* (NULL = the context's
+ * own stream).
+ */
+#ifndef PSGD_H
+#define PSGD_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PSGD_ABI_VERSION 1
+
+typedef struct psgd_ctx psgd_ctx;
+
+/* Gradient plugins -- [ext] Spark MLlib 1.6.1 Gradient.scala; called at PSGD.scala:254. */
+enum psgd_gradient {
+    PSGD_GRADIENT_LOGISTIC = 0,      /* LogisticGradient(numClasses = 2) */
+    PSGD_GRADIENT_LEAST_SQUARES = 1, /* LeastSquaresGradient */
+    PSGD_GRADIENT_HINGE = 2          /* HingeGradient */
+};
+
+/* Updater plugins -- UPD.scala:40-286; called at PSGD.scala:255. */
+enum psgd_updater {
+    PSGD_UPDATER_SIMPLE = 0,     /* SimpleSGDUpdater      UPD.scala:80-99   */
+    PSGD_UPDATER_SQUARED_L2 = 1, /* SquaredL2SGDUpdater   UPD.scala:157-182 */
+    PSGD_UPDATER_L1 = 2,         /* L1SGDUpdater          UPD.scala:120-149 */
+    PSGD_UPDATER_ADAGRAD = 3,    /* AdaGradSGDUpdater     UPD.scala:193-228 */
+    PSGD_UPDATER_ADAM = 4        /* AdamSGDUpdater        UPD.scala:240-286 */
+};
+
+/* Element types. Storage dtype is chosen per registered partition; compute dtype per epoch:
+ * PSGD_F64 reproduces the reference's double arithmetic (parity mode); PSGD_F32 computes the
+ * chain in float (throughput mode, looser stated tolerance). */
+enum psgd_dtype { PSGD_F64 = 0, PSGD_F32 = 1 };
+
+enum psgd_status {
+    PSGD_OK = 0,
+    PSGD_EINVAL = -1,       /* bad argument (IllegalArgumentException) */
+    PSGD_EUNSUPPORTED = -2, /* valid in the reference, not built here yet */
+    PSGD_EDEVICE = -3,      /* HIP runtime failure */
+    PSGD_ENOMEM = -4,
+    PSGD_ESTATE = -5        /* call sequence error (e.g. no partitions registered) */
+};
+
+/* Hyper-parameters of one outer iteration (ParallelizedSGD.scala:46-50 defaults; validation
+ * mirrors the setters' `require`s at :57-113). */
+typedef struct {
+    int32_t gradient;           /* enum psgd_gradient */
+    int32_t updater;            /* enum psgd_updater */
+    int32_t compute_dtype;      /* enum psgd_dtype */
+    int32_t iteration;          /* outer iteration i (1-based), sampling seed 42+i (PSGD:242) */
+    double step_size;           /* stepSize > 0 */
+    double reg_param;           /* regParam >= 0 */
+    double mini_batch_fraction; /* (0, 1]; only 1.0 is built (RDD.sample is then the identity) */
+    double convergence_tol;     /* [0, 1]; 0 disables the per-sample break (PSGD.scala:262) */
+    double adam_beta, adam_gamma, adam_eps; /* AdamSGDUpdater(beta, gamma, eps), UPD:241-244 */
+} psgd_params;
+
+int32_t psgd_abi_version(void);
+const char* psgd_last_error(void);
+
+/* Context: one device, its stream, the partition registry and all device buffers. */
+int32_t psgd_ctx_create(int32_t device, psgd_ctx** out);
+int32_t psgd_ctx_destroy(psgd_ctx* ctx);
+
+/* Register partition `part` (its index in the RDD = its chain id) from host memory; the data
+ * is copied to HBM once (the analogue of RDD.cache(), ParallelizedSGDSuite.scala:88) and no host
+ * pointer is kept. Rows are in the partition's iterator order. labels[n_rows] are doubles;
+ * x is row-major n_rows x d of `dtype`. Thread-safe (Spark local[N] registers from N task
+ * threads). Empty partitions (n_rows == 0) must be registered too: they take part in the
+ * combine with count 0 (PSGD.scala:270-276). Replaces the mapPartitions closure input at
+ * PSGD.scala:243-253. */
+int32_t psgd_register_dense(psgd_ctx* ctx, int64_t part, int64_t n_rows, int32_t d,
+                            const double* labels, const void* x, int32_t dtype);
+
+/* Same for CSR rows: row_ptr[n_rows+1] (row_ptr[0] may be non-zero), col[] strictly
+ * increasing within a row and < d, val[] of `dtype` (MLlib SparseVector rows). */
+int32_t psgd_register_csr(psgd_ctx* ctx, int64_t part, int64_t n_rows, int32_t d,
+                          const double* labels, const int64_t* row_ptr, const int32_t* col,
+                          const void* val, int32_t dtype);
+
+/* Zero-copy registration of a dense partition already resident on the context's device:
+ * d_x row-major with leading dimension ld >= d elements (16-byte aligned rows; columns
+ * [d, ld) must hold zeros), d_labels[n_rows]. The caller keeps both alive. */
+int32_t psgd_register_dense_device(psgd_ctx* ctx, int64_t part, int64_t n_rows, int32_t d,
+                                   int64_t ld, const double* d_labels, const void* d_x,
+                                   int32_t dtype);
+
+int32_t psgd_clear_partitions(psgd_ctx* ctx);
+int32_t psgd_num_partitions(psgd_ctx* ctx, int64_t* n_parts, int64_t* n_rows_total);
+
+/* One outer iteration over this process's partitions (PSGD.scala:238-276):
+ * every chain starts from w_in (the broadcast, :238/:245), runs its partition in iterator
+ * order with j restarting at 1 (:243-269), and the chains' (w, regVal, lossSum, count) are
+ * folded with the reference's combiner (:271-276) in partition-index order.
+ * Host pointers: w_in[d] -> w_out[d] (the fold's averaged weights), *regval_out, *loss_sum_out,
+ * *count_out; chain_counts[n_parts] (nullable) receives each chain's processed count.
+ * A count of 0 means an empty batch (:295-297): the caller keeps its weights. */
+int32_t psgd_run_epoch(psgd_ctx* ctx, const psgd_params* params, const double* w_in,
+                       double* w_out, double* regval_out, double* loss_sum_out,
+                       int64_t* count_out, int64_t* chain_counts);
+
+/* Device-resident form of psgd_run_epoch for hosts that keep the weights in HBM across
+ * iterations (the broadcast at PSGD.scala:238 disappears): d_w_in[d] on the device;
+ * d_partial[d+3] receives {w_avg[0..d), regVal, lossSum, (double)count}; d_chain_counts
+ * (nullable) [n_parts] int64. Enqueued on `stream`; no host synchronisation. */
+int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const double* d_w_in,
+                              double* d_partial, int64_t* d_chain_counts, void* stream);
+
+/* Fold n per-process partials (each d+3 doubles, laid out back to back, in rank order) with
+ * the reference's combiner (PSGD.scala:271-276) into d_out[d+3]: the cross-GPU level of the
+ * treeReduce, applied after an all-gather of the partials. */
+int32_t psgd_fold_partials_device(psgd_ctx* ctx, int32_t n, int32_t d, const double* d_partials,
+                                  double* d_out, void* stream);
+
+/* Driver-side isConverged terms (PSGD.scala:289-294, :324-336): writes
+ * {sum((prev-cur)^2), sum(cur^2)} to h_out[2] (host) after synchronising `stream`. */
+int32_t psgd_convergence_terms_device(psgd_ctx* ctx, int32_t d, const double* d_prev,
+                                      const double* d_cur, double* h_out, void* stream);
+
+/* Updater regVal at iteration 0 (PSGD.scala:231-233): updater.compute(w, 0, 0, 1, reg)._2 for
+ * host weights w[d], computed on the context's device. */
+int32_t psgd_initial_regval(psgd_ctx* ctx, const psgd_params* params, int32_t d, const double* w,
+                            double* regval_out);
+
+/* Diagnostics: which chain kernel the last epoch launched (101/102/104/108 = register-resident
+ * dense kernel with NV 16-byte vectors per lane; 200 = general dense; 201 = general CSR). */
+int32_t psgd_ctx_last_kernel(psgd_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PSGD_H */

@@ -159,6 +159,11 @@ def _signum(x: float) -> float:
     return 1.0 if x > 0.0 else -1.0
 
 
+def _jsqrt(x: float) -> float:
+    """Math.pow(x, 0.5) / Math.sqrt: NaN (not an exception) for negative x."""
+    return math.sqrt(x) if x >= 0 else math.nan
+
+
 def log1p_exp(x: float) -> float:
     """[ext] MLlib 1.6.1 MLUtils.log1pExp."""
     if x > 0:
@@ -283,7 +288,7 @@ def updater(kind: int, w, g, step: float, it: int, reg: float, st: UpdaterState,
         sq = [v * v for v in gd]
         st.a = sq if st.a is None else [st.a[i] + sq[i] for i in range(d)]
         for i in range(d):
-            w[i] = w[i] + (-s) * (gd[i] / math.sqrt(st.a[i] + 1.0))
+            w[i] = w[i] + (-s) * (gd[i] / _jsqrt(st.a[i] + 1.0))
         return 0.0
     if kind == UPD_ADAM:
         sq = [v * v for v in gd]
@@ -295,7 +300,7 @@ def updater(kind: int, w, g, step: float, it: int, reg: float, st: UpdaterState,
             st.b = [st.b[i] * gamma + sq[i] * (1 - gamma) for i in range(d)]
         lr = s / (1.0 - math.pow(beta, float(it)))
         for i in range(d):
-            fix1 = math.sqrt(1.0 - math.pow(st.b[i], float(it))) + eps
+            fix1 = _jsqrt(1.0 - math.pow(st.b[i], float(it))) + eps
             w[i] = w[i] + (-lr) * (st.a[i] / fix1)
         return 0.0
     raise ValueError(kind)

@@ -1,0 +1,610 @@
+// psgd_capi.cpp -- the C ABI declared in include/psgd.h: context, partition registry, epoch
+// orchestration and error reporting. The chain/fold kernels live in psgd_kernels.hip.
+//
+// What this replaces in the reference (paths under /root/reference,
+// src/main/scala/org/apache/spark/mllib/optimization/ParallelizedSGD.scala):
+//   :238      sc.broadcast(weights)            -> weights stay in HBM (d_w_in)
+//   :242      data.sample(false, frac, 42+i)   -> identity for frac >= 1 - 1e-6 (Spark's
+//                                                 RandomSampler.roundingEpsilon), empty for
+//                                                 frac <= 1e-6; otherwise PSGD_EUNSUPPORTED
+//   :243-270  mapPartitions chain              -> one chain kernel launch over all partitions
+//   :271-276  treeReduce combiner              -> fold kernel in partition-index order
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/psgd.h"
+#include "psgd_internal.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int32_t fail(int32_t code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return fail(PSGD_EDEVICE, std::string("HIP error in ") + #expr + ": " +          \
+                                          hipGetErrorString(e_));                            \
+    } while (0)
+
+size_t dtype_size(int32_t dt) { return dt == PSGD_F32 ? 4 : 8; }
+
+struct Part {
+    int64_t n_rows = 0;
+    int32_t d = 0;
+    int32_t dtype = PSGD_F64;
+    int32_t layout = psgd::kDense;
+    bool owned = false;
+    void* x = nullptr;        // dense rows or CSR values
+    double* y = nullptr;
+    int64_t* row_ptr = nullptr;
+    int32_t* col = nullptr;
+    int64_t ld = 0;
+};
+
+// Device buffer that only grows.
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t need) {
+        if (need <= bytes) return hipSuccess;
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipMalloc(&p, need);
+        if (e == hipSuccess) bytes = need;
+        return e;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <typename T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+}  // namespace
+
+struct psgd_ctx {
+    int32_t device = 0;
+    int32_t num_cus = 256;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    std::map<int64_t, Part> parts;
+    bool descs_dirty = true;
+    DevBuf descs, w_in, w_out, state, rv, loss, cnt_d, cnt, steps, partial, tmp;
+    double steps_value = NAN;
+    int64_t steps_n = 0;
+    int32_t last_variant = 0;
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        hipGetDevice(&prev);
+        if (prev != dev) hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        hipGetDevice(&cur);
+        if (prev >= 0 && cur != prev) hipSetDevice(prev);
+    }
+};
+
+void free_part(Part& p) {
+    if (!p.owned) return;
+    if (p.x) hipFree(p.x);
+    if (p.y) hipFree(p.y);
+    if (p.row_ptr) hipFree(p.row_ptr);
+    if (p.col) hipFree(p.col);
+    p = Part{};
+}
+
+int32_t check_compat(psgd_ctx* ctx, int32_t d, int32_t dtype, int32_t layout) {
+    for (auto& kv : ctx->parts) {
+        const Part& q = kv.second;
+        if (q.d != d)
+            return fail(PSGD_EINVAL, "requirement failed: all partitions must have the same "
+                                     "number of features (got " + std::to_string(d) + " and " +
+                                         std::to_string(q.d) + ")");
+        if (q.dtype != dtype || q.layout != layout)
+            return fail(PSGD_EUNSUPPORTED,
+                        "mixing dense/CSR rows or storage dtypes across partitions is not built");
+    }
+    return PSGD_OK;
+}
+
+int32_t validate_params(const psgd_params* p) {
+    if (!p) return fail(PSGD_EINVAL, "params is null");
+    if (p->gradient < PSGD_GRADIENT_LOGISTIC || p->gradient > PSGD_GRADIENT_HINGE)
+        return fail(PSGD_EINVAL, "unknown gradient kind " + std::to_string(p->gradient));
+    if (p->updater < PSGD_UPDATER_SIMPLE || p->updater > PSGD_UPDATER_ADAM)
+        return fail(PSGD_EINVAL, "unknown updater kind " + std::to_string(p->updater));
+    if (p->compute_dtype != PSGD_F64 && p->compute_dtype != PSGD_F32)
+        return fail(PSGD_EINVAL, "unknown compute dtype " + std::to_string(p->compute_dtype));
+    // Spark 1.6.1 BernoulliSampler: require(fraction in [0 - eps, 1 + eps]) [ext].
+    const double eps = 1e-6;
+    if (!(p->mini_batch_fraction >= -eps && p->mini_batch_fraction <= 1.0 + eps)) {
+        char buf[160];
+        snprintf(buf, sizeof buf, "requirement failed: Sampling fraction (%g) must be on interval [0, 1]",
+                 p->mini_batch_fraction);
+        return fail(PSGD_EINVAL, buf);
+    }
+    if (p->mini_batch_fraction > eps && p->mini_batch_fraction < 1.0 - eps)
+        return fail(PSGD_EUNSUPPORTED,
+                    "miniBatchFraction < 1.0 (Bernoulli sampling, ParallelizedSGD.scala:242) is "
+                    "not built yet");
+    return PSGD_OK;
+}
+
+// Allocate per-chain buffers and upload descriptors (ctx->mu held).
+int32_t prepare(psgd_ctx* ctx, int32_t d, bool need_state, hipStream_t st) {
+    const size_t P = ctx->parts.size();
+    HIP_TRY(ctx->descs.ensure(std::max<size_t>(P, 1) * sizeof(psgd::ChainDesc)));
+    HIP_TRY(ctx->w_in.ensure((size_t)std::max(d, 1) * sizeof(double)));
+    HIP_TRY(ctx->w_out.ensure(std::max<size_t>(P, 1) * (size_t)std::max(d, 1) * sizeof(double)));
+    HIP_TRY(ctx->rv.ensure(std::max<size_t>(P, 1) * sizeof(double)));
+    HIP_TRY(ctx->loss.ensure(std::max<size_t>(P, 1) * sizeof(double)));
+    HIP_TRY(ctx->cnt_d.ensure(std::max<size_t>(P, 1) * sizeof(double)));
+    HIP_TRY(ctx->cnt.ensure(std::max<size_t>(P, 1) * sizeof(int64_t)));
+    HIP_TRY(ctx->partial.ensure(((size_t)std::max(d, 1) + 3) * sizeof(double)));
+    HIP_TRY(ctx->tmp.ensure(((size_t)std::max(d, 1) + 8) * sizeof(double)));
+    if (need_state)
+        HIP_TRY(ctx->state.ensure(std::max<size_t>(P, 1) * 2 * (size_t)std::max(d, 1) *
+                                  sizeof(double)));
+    if (ctx->descs_dirty) {
+        std::vector<psgd::ChainDesc> h;
+        h.reserve(P);
+        for (auto& kv : ctx->parts) {
+            const Part& q = kv.second;
+            psgd::ChainDesc c;
+            c.x = q.x;
+            c.y = q.y;
+            c.row_ptr = q.row_ptr;
+            c.col = q.col;
+            c.n_rows = q.n_rows;
+            c.ld = q.ld;
+            h.push_back(c);
+        }
+        if (P) {
+            HIP_TRY(hipMemcpyAsync(ctx->descs.p, h.data(), P * sizeof(psgd::ChainDesc),
+                                   hipMemcpyHostToDevice, st));
+            HIP_TRY(hipStreamSynchronize(st));
+        }
+        ctx->descs_dirty = false;
+    }
+    return PSGD_OK;
+}
+
+int32_t ensure_steps(psgd_ctx* ctx, double step, int64_t n, hipStream_t st) {
+    n = std::max<int64_t>(n, 1);
+    if (ctx->steps_n >= n && ctx->steps_value == step) return PSGD_OK;
+    HIP_TRY(ctx->steps.ensure((size_t)n * sizeof(double)));
+    int e = psgd::launch_steps(step, n, ctx->steps.as<double>(), st);
+    if (e) return fail(PSGD_EDEVICE, "steps kernel launch failed");
+    ctx->steps_value = step;
+    ctx->steps_n = n;
+    return PSGD_OK;
+}
+
+// Dynamic LDS request used only to spread chains evenly over the CUs (a CU admits
+// floor(160 KiB / request) chain workgroups). PSGD_LDS_SPREAD=0 disables it.
+int lds_spread_bytes(const psgd_ctx* ctx, size_t P) {
+    const char* env = getenv("PSGD_LDS_SPREAD");
+    if (env) return std::max(0, atoi(env));
+    if (P == 0) return 0;
+    const size_t per_cu = (P + (size_t)ctx->num_cus - 1) / (size_t)ctx->num_cus;
+    if (per_cu > 8) return 0;
+    const size_t lds_total = 160 * 1024;
+    size_t want = lds_total / (per_cu + 1) + 1024;  // per_cu fit, per_cu + 1 do not
+    want = std::min<size_t>(want, 64 * 1024);
+    return (int)(want & ~(size_t)1023);
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t psgd_abi_version(void) { return PSGD_ABI_VERSION; }
+
+const char* psgd_last_error(void) { return g_last_error.c_str(); }
+
+int32_t psgd_ctx_create(int32_t device, psgd_ctx** out) {
+    if (!out) return fail(PSGD_EINVAL, "out is null");
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0)
+        return fail(PSGD_EDEVICE, std::string("no HIP device available: ") + hipGetErrorString(e));
+    if (device < 0 || device >= n)
+        return fail(PSGD_EINVAL, "device index " + std::to_string(device) + " out of range");
+    DeviceGuard g(device);
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::string(prop.gcnArchName).rfind("gfx950", 0) != 0)
+        return fail(PSGD_EUNSUPPORTED, std::string("kernels are built for gfx950, device is ") +
+                                           prop.gcnArchName);
+    psgd_ctx* ctx = new psgd_ctx();
+    ctx->device = device;
+    ctx->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete ctx;
+        return fail(PSGD_EDEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+    }
+    *out = ctx;
+    return PSGD_OK;
+}
+
+int32_t psgd_ctx_destroy(psgd_ctx* ctx) {
+    if (!ctx) return PSGD_OK;
+    {
+        DeviceGuard g(ctx->device);
+        hipStreamSynchronize(ctx->stream);
+        for (auto& kv : ctx->parts) free_part(kv.second);
+        for (DevBuf* b : {&ctx->descs, &ctx->w_in, &ctx->w_out, &ctx->state, &ctx->rv, &ctx->loss,
+                          &ctx->cnt_d, &ctx->cnt, &ctx->steps, &ctx->partial, &ctx->tmp})
+            b->release();
+        hipStreamDestroy(ctx->stream);
+    }
+    delete ctx;
+    return PSGD_OK;
+}
+
+int32_t psgd_register_dense(psgd_ctx* ctx, int64_t part, int64_t n_rows, int32_t d,
+                            const double* labels, const void* x, int32_t dtype) {
+    if (!ctx) return fail(PSGD_EINVAL, "ctx is null");
+    if (part < 0) return fail(PSGD_EINVAL, "partition index must be non-negative");
+    if (n_rows < 0 || d <= 0) return fail(PSGD_EINVAL, "n_rows must be >= 0 and d > 0");
+    if (dtype != PSGD_F64 && dtype != PSGD_F32) return fail(PSGD_EINVAL, "unknown dtype");
+    if (n_rows > 0 && (!labels || !x)) return fail(PSGD_EINVAL, "labels/x are null");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DeviceGuard g(ctx->device);
+    int32_t rc = check_compat(ctx, d, dtype, psgd::kDense);
+    if (rc) return rc;
+    const size_t es = dtype_size(dtype);
+    const int64_t vec = (int64_t)(16 / es);
+    Part p;
+    p.n_rows = n_rows;
+    p.d = d;
+    p.dtype = dtype;
+    p.layout = psgd::kDense;
+    p.owned = true;
+    p.ld = (d + vec - 1) / vec * vec;
+    if (n_rows > 0) {
+        const size_t xbytes = (size_t)n_rows * (size_t)p.ld * es;
+        HIP_TRY(hipMalloc(&p.x, xbytes));
+        HIP_TRY(hipMalloc((void**)&p.y, (size_t)n_rows * sizeof(double)));
+        if (p.ld != d) HIP_TRY(hipMemsetAsync(p.x, 0, xbytes, ctx->stream));
+        HIP_TRY(hipMemcpy2DAsync(p.x, (size_t)p.ld * es, x, (size_t)d * es, (size_t)d * es,
+                                 (size_t)n_rows, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(p.y, labels, (size_t)n_rows * sizeof(double),
+                               hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+    }
+    auto it = ctx->parts.find(part);
+    if (it != ctx->parts.end()) free_part(it->second);
+    ctx->parts[part] = p;
+    ctx->descs_dirty = true;
+    return PSGD_OK;
+}
+
+int32_t psgd_register_dense_device(psgd_ctx* ctx, int64_t part, int64_t n_rows, int32_t d,
+                                   int64_t ld, const double* d_labels, const void* d_x,
+                                   int32_t dtype) {
+    if (!ctx) return fail(PSGD_EINVAL, "ctx is null");
+    if (part < 0) return fail(PSGD_EINVAL, "partition index must be non-negative");
+    if (n_rows < 0 || d <= 0 || ld < d) return fail(PSGD_EINVAL, "need n_rows >= 0, d > 0, ld >= d");
+    if (dtype != PSGD_F64 && dtype != PSGD_F32) return fail(PSGD_EINVAL, "unknown dtype");
+    const size_t es = dtype_size(dtype);
+    if (((size_t)ld * es) % 16 != 0 || ((uintptr_t)d_x % 16) != 0)
+        return fail(PSGD_EINVAL, "device rows must be 16-byte aligned (ld * sizeof(dtype) % 16 == 0)");
+    if (n_rows > 0 && (!d_labels || !d_x)) return fail(PSGD_EINVAL, "labels/x are null");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    int32_t rc = check_compat(ctx, d, dtype, psgd::kDense);
+    if (rc) return rc;
+    Part p;
+    p.n_rows = n_rows;
+    p.d = d;
+    p.dtype = dtype;
+    p.layout = psgd::kDense;
+    p.owned = false;
+    p.x = const_cast<void*>(d_x);
+    p.y = const_cast<double*>(d_labels);
+    p.ld = ld;
+    auto it = ctx->parts.find(part);
+    if (it != ctx->parts.end()) free_part(it->second);
+    ctx->parts[part] = p;
+    ctx->descs_dirty = true;
+    return PSGD_OK;
+}
+
+int32_t psgd_register_csr(psgd_ctx* ctx, int64_t part, int64_t n_rows, int32_t d,
+                          const double* labels, const int64_t* row_ptr, const int32_t* col,
+                          const void* val, int32_t dtype) {
+    if (!ctx) return fail(PSGD_EINVAL, "ctx is null");
+    if (part < 0) return fail(PSGD_EINVAL, "partition index must be non-negative");
+    if (n_rows < 0 || d <= 0) return fail(PSGD_EINVAL, "n_rows must be >= 0 and d > 0");
+    if (dtype != PSGD_F64 && dtype != PSGD_F32) return fail(PSGD_EINVAL, "unknown dtype");
+    if (n_rows > 0 && (!labels || !row_ptr)) return fail(PSGD_EINVAL, "labels/row_ptr are null");
+    // Validate and rebase the row pointers.
+    std::vector<int64_t> rp((size_t)n_rows + 1, 0);
+    const int64_t base = n_rows > 0 ? row_ptr[0] : 0;
+    for (int64_t r = 0; r <= n_rows; ++r) {
+        rp[(size_t)r] = row_ptr[r] - base;
+        if (r > 0 && rp[(size_t)r] < rp[(size_t)r - 1])
+            return fail(PSGD_EINVAL, "row_ptr must be non-decreasing");
+    }
+    const int64_t nnz = rp[(size_t)n_rows];
+    if (nnz > 0 && (!col || !val)) return fail(PSGD_EINVAL, "col/val are null");
+    for (int64_t r = 0; r < n_rows; ++r) {
+        for (int64_t k = rp[(size_t)r]; k < rp[(size_t)r + 1]; ++k) {
+            const int32_t c = col[base + k];
+            if (c < 0 || c >= d)
+                return fail(PSGD_EINVAL, "requirement failed: column index " + std::to_string(c) +
+                                             " out of range [0, " + std::to_string(d) + ")");
+            if (k > rp[(size_t)r] && c <= col[base + k - 1])
+                return fail(PSGD_EINVAL, "column indices must be strictly increasing within a row");
+        }
+    }
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DeviceGuard g(ctx->device);
+    int32_t rc = check_compat(ctx, d, dtype, psgd::kCsr);
+    if (rc) return rc;
+    const size_t es = dtype_size(dtype);
+    Part p;
+    p.n_rows = n_rows;
+    p.d = d;
+    p.dtype = dtype;
+    p.layout = psgd::kCsr;
+    p.owned = true;
+    if (n_rows > 0) {
+        HIP_TRY(hipMalloc((void**)&p.row_ptr, rp.size() * sizeof(int64_t)));
+        HIP_TRY(hipMalloc((void**)&p.y, (size_t)n_rows * sizeof(double)));
+        HIP_TRY(hipMemcpyAsync(p.row_ptr, rp.data(), rp.size() * sizeof(int64_t),
+                               hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(p.y, labels, (size_t)n_rows * sizeof(double),
+                               hipMemcpyHostToDevice, ctx->stream));
+        if (nnz > 0) {
+            HIP_TRY(hipMalloc((void**)&p.col, (size_t)nnz * sizeof(int32_t)));
+            HIP_TRY(hipMalloc(&p.x, (size_t)nnz * es));
+            HIP_TRY(hipMemcpyAsync(p.col, col + base, (size_t)nnz * sizeof(int32_t),
+                                   hipMemcpyHostToDevice, ctx->stream));
+            HIP_TRY(hipMemcpyAsync(p.x, static_cast<const char*>(val) + (size_t)base * es,
+                                   (size_t)nnz * es, hipMemcpyHostToDevice, ctx->stream));
+        }
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+    }
+    auto it = ctx->parts.find(part);
+    if (it != ctx->parts.end()) free_part(it->second);
+    ctx->parts[part] = p;
+    ctx->descs_dirty = true;
+    return PSGD_OK;
+}
+
+int32_t psgd_clear_partitions(psgd_ctx* ctx) {
+    if (!ctx) return fail(PSGD_EINVAL, "ctx is null");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DeviceGuard g(ctx->device);
+    hipStreamSynchronize(ctx->stream);
+    for (auto& kv : ctx->parts) free_part(kv.second);
+    ctx->parts.clear();
+    ctx->descs_dirty = true;
+    return PSGD_OK;
+}
+
+int32_t psgd_num_partitions(psgd_ctx* ctx, int64_t* n_parts, int64_t* n_rows_total) {
+    if (!ctx) return fail(PSGD_EINVAL, "ctx is null");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    int64_t rows = 0;
+    for (auto& kv : ctx->parts) rows += kv.second.n_rows;
+    if (n_parts) *n_parts = (int64_t)ctx->parts.size();
+    if (n_rows_total) *n_rows_total = rows;
+    return PSGD_OK;
+}
+
+int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const double* d_w_in,
+                              double* d_partial, int64_t* d_chain_counts, void* stream) {
+    if (!ctx) return fail(PSGD_EINVAL, "ctx is null");
+    int32_t rc = validate_params(params);
+    if (rc) return rc;
+    if (!d_w_in || !d_partial) return fail(PSGD_EINVAL, "d_w_in/d_partial are null");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (ctx->parts.empty()) return fail(PSGD_ESTATE, "no partitions registered");
+    DeviceGuard g(ctx->device);
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    const Part& first = ctx->parts.begin()->second;
+    const int32_t d = first.d;
+    const int32_t layout = first.layout;
+    const bool stateful = params->updater == PSGD_UPDATER_ADAGRAD || params->updater == PSGD_UPDATER_ADAM;
+    const bool conv = params->convergence_tol > 0.0;
+    if (layout == psgd::kCsr && stateful)
+        return fail(PSGD_EUNSUPPORTED, "CSR rows with AdaGrad/Adam updaters are not built yet");
+    const bool need_state = stateful || (layout == psgd::kCsr && conv);
+    rc = prepare(ctx, d, need_state, st);
+    if (rc) return rc;
+    int64_t n_max = 0, max_ld = 0, min_ld = INT64_MAX;
+    for (auto& kv : ctx->parts) {
+        n_max = std::max(n_max, kv.second.n_rows);
+        if (kv.second.n_rows > 0) {
+            max_ld = std::max(max_ld, kv.second.ld);
+            min_ld = std::min(min_ld, kv.second.ld);
+        }
+    }
+    if (max_ld == 0) max_ld = min_ld = d;
+    const bool sample_empty = params->mini_batch_fraction <= 1e-6;
+    rc = ensure_steps(ctx, params->step_size, n_max, st);
+    if (rc) return rc;
+
+    const int P = (int)ctx->parts.size();
+    psgd::ChainLaunch L;
+    L.descs = ctx->descs.as<psgd::ChainDesc>();
+    L.w_in = d_w_in;
+    L.w_out = ctx->w_out.as<double>();
+    L.state = need_state ? ctx->state.as<double>() : nullptr;
+    L.rv = ctx->rv.as<double>();
+    L.loss = ctx->loss.as<double>();
+    L.cnt_d = ctx->cnt_d.as<double>();
+    L.cnt = ctx->cnt.as<int64_t>();
+    L.steps = ctx->steps.as<double>();
+    psgd::KParams kp;
+    kp.reg = params->reg_param;
+    kp.tol = params->convergence_tol;
+    kp.beta = params->adam_beta;
+    kp.gamma = params->adam_gamma;
+    kp.eps = params->adam_eps;
+    kp.d = d;
+    kp.n_chains = P;
+
+    if (sample_empty) {
+        // RDD.sample with fraction 0: every partition is empty -> (w_in, 0, 0, 0) per chain.
+        for (int p = 0; p < P; ++p)
+            HIP_TRY(hipMemcpyAsync(L.w_out + (size_t)p * d, d_w_in, (size_t)d * sizeof(double),
+                                   hipMemcpyDeviceToDevice, st));
+        HIP_TRY(hipMemsetAsync(L.rv, 0, P * sizeof(double), st));
+        HIP_TRY(hipMemsetAsync(L.loss, 0, P * sizeof(double), st));
+        HIP_TRY(hipMemsetAsync(L.cnt_d, 0, P * sizeof(double), st));
+        HIP_TRY(hipMemsetAsync(L.cnt, 0, P * sizeof(int64_t), st));
+    } else {
+        int e = psgd::launch_chains(L, kp, layout, first.dtype == PSGD_F32 ? 1 : 0,
+                                    params->compute_dtype == PSGD_F32 ? 1 : 0, params->gradient,
+                                    params->updater, conv, min_ld, max_ld,
+                                    lds_spread_bytes(ctx, (size_t)P), st, &ctx->last_variant);
+        if (e == -2) return fail(PSGD_EUNSUPPORTED, "this gradient/updater/layout combination is not built");
+        if (e) return fail(PSGD_EDEVICE, std::string("chain kernel launch failed: ") +
+                                             hipGetErrorString((hipError_t)e));
+    }
+    int e = psgd::launch_fold(L.w_out, d, L.rv, L.loss, L.cnt_d, 1, P, d, d_partial, st);
+    if (e) return fail(PSGD_EDEVICE, "fold kernel launch failed");
+    if (d_chain_counts)
+        HIP_TRY(hipMemcpyAsync(d_chain_counts, L.cnt, (size_t)P * sizeof(int64_t),
+                               hipMemcpyDeviceToDevice, st));
+    return PSGD_OK;
+}
+
+int32_t psgd_run_epoch(psgd_ctx* ctx, const psgd_params* params, const double* w_in,
+                       double* w_out, double* regval_out, double* loss_sum_out,
+                       int64_t* count_out, int64_t* chain_counts) {
+    if (!ctx) return fail(PSGD_EINVAL, "ctx is null");
+    if (!w_in || !w_out) return fail(PSGD_EINVAL, "w_in/w_out are null");
+    int32_t d = 0;
+    size_t P = 0;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        if (ctx->parts.empty()) return fail(PSGD_ESTATE, "no partitions registered");
+        d = ctx->parts.begin()->second.d;
+        P = ctx->parts.size();
+        DeviceGuard g(ctx->device);
+        HIP_TRY(ctx->w_in.ensure((size_t)d * sizeof(double)));
+        HIP_TRY(ctx->partial.ensure(((size_t)d + 3) * sizeof(double)));
+        HIP_TRY(ctx->tmp.ensure(((size_t)d + 8) * sizeof(double)));
+        HIP_TRY(hipMemcpyAsync(ctx->w_in.p, w_in, (size_t)d * sizeof(double),
+                               hipMemcpyHostToDevice, ctx->stream));
+    }
+    int64_t* d_counts = nullptr;
+    DevBuf counts;
+    DeviceGuard g(ctx->device);
+    if (chain_counts) {
+        HIP_TRY(counts.ensure(P * sizeof(int64_t)));
+        d_counts = counts.as<int64_t>();
+    }
+    int32_t rc = psgd_run_epoch_device(ctx, params, ctx->w_in.as<double>(),
+                                       ctx->partial.as<double>(), d_counts, ctx->stream);
+    if (rc) {
+        counts.release();
+        return rc;
+    }
+    std::vector<double> h((size_t)d + 3);
+    HIP_TRY(hipMemcpyAsync(h.data(), ctx->partial.p, h.size() * sizeof(double),
+                           hipMemcpyDeviceToHost, ctx->stream));
+    if (chain_counts)
+        HIP_TRY(hipMemcpyAsync(chain_counts, d_counts, P * sizeof(int64_t), hipMemcpyDeviceToHost,
+                               ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    counts.release();
+    std::memcpy(w_out, h.data(), (size_t)d * sizeof(double));
+    if (regval_out) *regval_out = h[(size_t)d];
+    if (loss_sum_out) *loss_sum_out = h[(size_t)d + 1];
+    if (count_out) *count_out = (int64_t)h[(size_t)d + 2];
+    return PSGD_OK;
+}
+
+int32_t psgd_fold_partials_device(psgd_ctx* ctx, int32_t n, int32_t d, const double* d_partials,
+                                  double* d_out, void* stream) {
+    if (!ctx) return fail(PSGD_EINVAL, "ctx is null");
+    if (n <= 0 || d <= 0 || !d_partials || !d_out) return fail(PSGD_EINVAL, "bad fold arguments");
+    DeviceGuard g(ctx->device);
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    const int64_t stride = (int64_t)d + 3;
+    int e = psgd::launch_fold(d_partials, stride, d_partials + d, d_partials + d + 1,
+                              d_partials + d + 2, stride, n, d, d_out, st);
+    if (e) return fail(PSGD_EDEVICE, "fold kernel launch failed");
+    return PSGD_OK;
+}
+
+int32_t psgd_convergence_terms_device(psgd_ctx* ctx, int32_t d, const double* d_prev,
+                                      const double* d_cur, double* h_out, void* stream) {
+    if (!ctx) return fail(PSGD_EINVAL, "ctx is null");
+    if (d <= 0 || !d_prev || !d_cur || !h_out) return fail(PSGD_EINVAL, "bad arguments");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DeviceGuard g(ctx->device);
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    HIP_TRY(ctx->tmp.ensure(((size_t)d + 8) * sizeof(double)));
+    double* t = ctx->tmp.as<double>();
+    int e = psgd::launch_sq_terms(d_prev, d_cur, d, t, st);
+    if (e) return fail(PSGD_EDEVICE, "sq_terms kernel launch failed");
+    HIP_TRY(hipMemcpyAsync(h_out, t, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return PSGD_OK;
+}
+
+int32_t psgd_initial_regval(psgd_ctx* ctx, const psgd_params* params, int32_t d, const double* w,
+                            double* regval_out) {
+    if (!ctx) return fail(PSGD_EINVAL, "ctx is null");
+    int32_t rc = validate_params(params);
+    if (rc) return rc;
+    if (d <= 0 || !w || !regval_out) return fail(PSGD_EINVAL, "bad arguments");
+    if (params->updater != PSGD_UPDATER_SQUARED_L2 && params->updater != PSGD_UPDATER_L1) {
+        *regval_out = 0.0;  // Simple / AdaGrad / Adam return 0 (UPD.scala:97, :214, :267)
+        return PSGD_OK;
+    }
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DeviceGuard g(ctx->device);
+    HIP_TRY(ctx->tmp.ensure(((size_t)d + 8) * sizeof(double)));
+    double* t = ctx->tmp.as<double>();
+    HIP_TRY(hipMemcpyAsync(t + 8, w, (size_t)d * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    int e = psgd::launch_sq_terms(nullptr, t + 8, d, t, ctx->stream);
+    if (e) return fail(PSGD_EDEVICE, "sq_terms kernel launch failed");
+    double h[2];
+    HIP_TRY(hipMemcpyAsync(h, t, sizeof h, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (params->updater == PSGD_UPDATER_SQUARED_L2) {
+        // w' = w * (1 - 0*reg); rv = 0.5 * reg * norm * norm (UPD.scala:176-180)
+        const double nrm = std::sqrt(h[0]);
+        *regval_out = 0.5 * params->reg_param * nrm * nrm;
+    } else {
+        *regval_out = h[1] * params->reg_param;  // UPD.scala:147 with shrinkage 0
+    }
+    return PSGD_OK;
+}
+
+int32_t psgd_ctx_last_kernel(psgd_ctx* ctx) { return ctx ? ctx->last_variant : 0; }
+
+}  // extern "C"

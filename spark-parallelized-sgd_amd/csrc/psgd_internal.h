@@ -1,0 +1,55 @@
+// psgd_internal.h -- structures shared by the C-ABI layer (psgd_capi.cpp) and the HIP kernels
+// (psgd_kernels.hip). Not part of the public ABI (include/psgd.h is).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace psgd {
+
+// One chain = one registered partition (its RDD partition index is its chain id, PSGD.scala:243).
+struct ChainDesc {
+    const void* x;           // dense rows (storage dtype) or CSR values
+    const double* y;         // labels[n_rows]
+    const int64_t* row_ptr;  // CSR: absolute offsets into col/x, [n_rows+1]; null for dense
+    const int32_t* col;      // CSR column indices
+    int64_t n_rows;
+    int64_t ld;              // dense: leading dimension in elements (>= d, multiple of 16B/elt)
+};
+
+// Per-launch scalars (hyper-parameters of ParallelizedSGD, PSGD.scala:46-50).
+struct KParams {
+    double reg;
+    double tol;
+    double beta, gamma, eps;  // AdamSGDUpdater (UPD.scala:241-244)
+    int32_t d;
+    int32_t n_chains;
+};
+
+enum Layout { kDense = 0, kCsr = 1 };
+
+// Everything a chain launch needs (device pointers).
+struct ChainLaunch {
+    const ChainDesc* descs;  // [n_chains]
+    const double* w_in;      // [d]
+    double* w_out;           // [n_chains * d]   per-chain final weights (also the general
+                             //                  kernel's working copy)
+    double* state;           // [n_chains * 2 * d] AdaGrad/Adam status (general kernel) or null
+    double* rv;              // [n_chains]  localRegVal
+    double* loss;            // [n_chains]  localLossSum
+    double* cnt_d;           // [n_chains]  count as double (exact < 2^53) for the fold
+    int64_t* cnt;            // [n_chains]  count
+    const double* steps;     // [n_max] stepSize / sqrt(j), j = 1..n_max
+};
+
+// Host-side launchers implemented in psgd_kernels.hip. Return hipError_t as int.
+// storage: 0 = f64, 1 = f32; compute: 0 = f64, 1 = f32.
+int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int storage, int compute,
+                  int gradient, int updater, bool check_conv, int64_t min_ld, int64_t max_ld,
+                  int lds_spread, hipStream_t stream, int* kernel_variant);
+int launch_fold(const double* w, int64_t w_stride, const double* rv, const double* loss,
+                const double* cnt, int64_t s_stride, int n, int d, double* out,
+                hipStream_t stream);
+int launch_sq_terms(const double* a, const double* b, int d, double* out2, hipStream_t stream);
+int launch_steps(double step, int64_t n, double* steps, hipStream_t stream);
+
+}  // namespace psgd

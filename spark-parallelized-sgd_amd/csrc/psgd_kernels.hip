@@ -1,0 +1,842 @@
+// psgd_kernels.hip -- CDNA4 (gfx950) kernels for the parallelized-SGD hot path.
+//
+// Reference (paths under /root/reference, src/main/scala/org/apache/spark/mllib/optimization/):
+//   chain loop      ParallelizedSGD.scala:243-270   -> chain_dense_reg / chain_general
+//   gradients       [ext] MLlib 1.6.1 Gradient.scala (called at ParallelizedSGD.scala:254)
+//   updaters        SGDUpdater.scala:86-98, :126-148, :163-181, :199-227, :252-285
+//   isConverged     ParallelizedSGD.scala:324-336 (per-sample form at :262)
+//   combine         ParallelizedSGD.scala:271-276   -> fold_kernel
+//
+// Mapping: one wavefront64 = one chain (= one RDD partition). The chain is sequential in its
+// samples; parallelism comes from the chains (one per CU) and, inside a chain, from the feature
+// dimension spread over the 64 lanes. Per sample: a d-long dot reduced across the wave with
+// DPP row ops + gfx950 permlane16/32 swaps (all lanes end with the bit-identical sum), the
+// gradient's scalar multiplier, and the updater's elementwise update, all in registers.
+// No MFMA: per-sample GEMV + axpy is not a dense contraction.
+//
+// Arithmetic follows the reference operator by operator (this file is compiled with
+// -ffp-contract=off): grad_i = mult * x_i, then w_i = w_i + (-s) * grad_i (Breeze axpy over
+// the MLlib gradient), L2 scaling w_i * (1 - s*lambda) before it. Only the dot product and the
+// norms are reassociated (wave tree instead of the F2J left fold), so fp64 mode agrees with the
+// reference to rounding, not bitwise.
+#include "psgd_internal.h"
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include <utility>
+
+namespace psgd {
+
+enum { G_LOGISTIC = 0, G_LEAST_SQUARES = 1, G_HINGE = 2 };
+enum { U_SIMPLE = 0, U_SQUARED_L2 = 1, U_L1 = 2, U_ADAGRAD = 3, U_ADAM = 4 };
+
+// ------------------------------------------------------------------------------------------
+// Wave-wide all-reduce. Every step adds a lane's value to its partner's (partners swap), so
+// each lane computes the same two operands in the same order and ends with the same bits.
+// ------------------------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+    long long b = __double_as_longlong(v);
+    int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, 0xF, 0xF, false);
+    int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// v_permlane16_swap / v_permlane32_swap (gfx950): with both operands = v, the pair returned
+// holds {value of the even partner, value of the odd partner} in every lane.
+__device__ __forceinline__ float swap_sum16(float v) {
+    auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(p[0]) + __uint_as_float(p[1]);
+}
+__device__ __forceinline__ float swap_sum32(float v) {
+    auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(p[0]) + __uint_as_float(p[1]);
+}
+__device__ __forceinline__ double swap_sum16(double v) {
+    unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32);
+    auto pl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    auto ph = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    double e = __longlong_as_double((long long)(((unsigned long long)ph[0] << 32) | pl[0]));
+    double o = __longlong_as_double((long long)(((unsigned long long)ph[1] << 32) | pl[1]));
+    return e + o;
+}
+__device__ __forceinline__ double swap_sum32(double v) {
+    unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32);
+    auto pl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    auto ph = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    double e = __longlong_as_double((long long)(((unsigned long long)ph[0] << 32) | pl[0]));
+    double o = __longlong_as_double((long long)(((unsigned long long)ph[1] << 32) | pl[1]));
+    return e + o;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+    v = v + dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+    v = v + dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+    v = v + dpp_mov<0x141>(v);  // row_half_mirror
+    v = v + dpp_mov<0x140>(v);  // row_mirror
+    v = swap_sum16(v);
+    v = swap_sum32(v);
+    return v;
+}
+
+// Two independent sums reduced together (ILP for the convergence terms).
+template <typename T>
+__device__ __forceinline__ void wave_sum2(T& a, T& b) {
+    a = a + dpp_mov<0xB1>(a);  b = b + dpp_mov<0xB1>(b);
+    a = a + dpp_mov<0x4E>(a);  b = b + dpp_mov<0x4E>(b);
+    a = a + dpp_mov<0x141>(a); b = b + dpp_mov<0x141>(b);
+    a = a + dpp_mov<0x140>(a); b = b + dpp_mov<0x140>(b);
+    a = swap_sum16(a);         b = swap_sum16(b);
+    a = swap_sum32(a);         b = swap_sum32(b);
+}
+
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+    long long b = __double_as_longlong(v);
+    int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
+    int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Global-address-space views: loads through them are global_load_* (in-order vmcnt) instead of
+// flat_load_* (which also count on lgkmcnt and force full drains before every use).
+template <typename T>
+using gptr = const T __attribute__((address_space(1)))*;
+template <typename T>
+using gmut = T __attribute__((address_space(1)))*;
+template <typename T>
+__device__ __forceinline__ gptr<T> as_global(const T* p) { return (gptr<T>)(p); }
+template <typename T>
+__device__ __forceinline__ gmut<T> as_global_mut(T* p) { return (gmut<T>)(p); }
+
+// ------------------------------------------------------------------------------------------
+// Scalar math per precision.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ double m_exp(double x) { return exp(x); }
+__device__ __forceinline__ float m_exp(float x) { return expf(x); }
+__device__ __forceinline__ double m_log1p(double x) { return log1p(x); }
+__device__ __forceinline__ float m_log1p(float x) { return log1pf(x); }
+__device__ __forceinline__ double m_sqrt(double x) { return sqrt(x); }
+__device__ __forceinline__ double m_fabs(double x) { return __builtin_fabs(x); }
+__device__ __forceinline__ float m_fabs(float x) { return __builtin_fabsf(x); }
+__device__ __forceinline__ float m_sqrt(float x) { return sqrtf(x); }
+__device__ __forceinline__ double m_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
+__device__ __forceinline__ float m_fma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+
+// java.lang.Math.max(a, b): NaN if either is NaN.
+template <typename T>
+__device__ __forceinline__ T jmax(T a, T b) {
+    return (a != a) ? a : ((b != b) ? b : (a >= b ? a : b));
+}
+// java.lang.Math.signum
+template <typename T>
+__device__ __forceinline__ T jsignum(T x) {
+    return (x != x || x == T(0)) ? x : (x > T(0) ? T(1) : T(-1));
+}
+
+// [ext] MLlib 1.6.1 MLUtils.log1pExp
+template <typename T>
+__device__ __forceinline__ T log1p_exp(T x) {
+    return x > T(0) ? x + m_log1p(m_exp(-x)) : m_log1p(m_exp(x));
+}
+
+// [ext] MLlib 1.6.1 Gradient.compute: the gradient is mult * x (Logistic: axpy(mult, x, 0);
+// LeastSquares: scal(diff, x.copy); Hinge: scal(-labelScaled, x.copy) or the empty vector,
+// which adds nothing -- mult = 0 gives the same weights). Returns loss.
+template <int GRAD, typename T>
+__device__ __forceinline__ T gradient_scalar(T z, T y, T& mult) {
+    if constexpr (GRAD == G_LOGISTIC) {
+        T margin = -z;                                    // -1.0 * dot(data, weights)
+        mult = (T(1) / (T(1) + m_exp(margin))) - y;
+        T l = log1p_exp(margin);
+        return y > T(0) ? l : l - margin;
+    } else if constexpr (GRAD == G_LEAST_SQUARES) {
+        T diff = z - y;
+        mult = diff;
+        return diff * diff / T(2);
+    } else {
+        T ls = T(2) * y - T(1);
+        T lz = ls * z;
+        bool on = T(1) > lz;
+        mult = on ? -ls : T(0);
+        return on ? T(1) - lz : T(0);
+    }
+}
+
+template <int... Is, typename F>
+__device__ __forceinline__ void static_for_impl(std::integer_sequence<int, Is...>, F&& f) {
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+// Calls f(std::integral_constant<int, i>) for i = 0..N-1: a guaranteed compile-time unroll.
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl(std::make_integer_sequence<int, N>{}, f);
+}
+
+template <typename S> struct Vec16;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+template <> struct Vec16<float> { using type = f32x4; static constexpr int N = 4; };
+template <> struct Vec16<double> { using type = f64x2; static constexpr int N = 2; };
+
+template <typename S, typename T>
+__device__ __forceinline__ void unpack(const typename Vec16<S>::type& v, T* out) {
+    if constexpr (Vec16<S>::N == 4) {
+        out[0] = T(v.x); out[1] = T(v.y); out[2] = T(v.z); out[3] = T(v.w);
+    } else {
+        out[0] = T(v.x); out[1] = T(v.y);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// chain_dense: dense rows, weights in VGPRs, rows streamed through an LDS ring.
+//
+// One workgroup = one chain = two waves on two SIMDs:
+//   wave 1 (loader)  streams the partition's rows, in iterator order, into an R-slot LDS ring
+//                    with global_load_lds (LDS DMA, 1 KiB per instruction, up to ~60 KiB in
+//                    flight), plus each row's label and stepSize/sqrt(j) (the "meta" bytes), and
+//                    publishes `ready` = number of rows that have landed;
+//   wave 0 (compute) owns the weights in registers and runs the sequential chain:
+//                    lane l, vector v (0..NV-1) owns features (v*64 + l)*VEC .. +VEC-1, so a
+//                    row slot is read with NV ds_read_b128 per lane; it publishes `consumed`.
+// Only the loader issues VMEM, so the compute wave never waits on vmcnt; the loader's LDS
+// accesses are inline asm so that the compiler does not drain its DMA before them.
+// ------------------------------------------------------------------------------------------
+struct RingHeader {
+    unsigned ready;     // rows landed in the ring (loader -> compute)
+    unsigned consumed;  // rows whose slot may be refilled (compute -> loader)
+    unsigned stop;      // compute wave left the chain early (per-sample convergence break)
+    unsigned pad;
+};
+constexpr int kMetaBytes = 256;  // one dword per lane of the meta DMA; bytes 0..15 = {y, step}
+
+__device__ __forceinline__ unsigned lds_load_u32_asm(const unsigned* p) {
+    unsigned v;
+    const unsigned addr = (unsigned)(uintptr_t)p;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
+    return v;
+}
+__device__ __forceinline__ void lds_store_u32_asm(unsigned* p, unsigned v) {
+    const unsigned addr = (unsigned)(uintptr_t)p;
+    asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : : "v"(addr), "v"(v) : "memory");
+}
+
+template <int NV>
+__device__ __forceinline__ constexpr int loader_depth() {
+    // rows in flight before the loader waits for the oldest: (NV + 1) VMEM instructions per
+    // row, vmcnt counts at most 63.
+    return 60 / (NV + 1);
+}
+
+template <typename S, typename T, int GRAD, int UPD, bool CONV, int NV, bool FULL>
+__global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, int ring_rows) {
+    using V = typename Vec16<S>::type;
+    constexpr int VEC = Vec16<S>::N;
+    constexpr int E = NV * VEC;
+    constexpr int ROW_BYTES = NV * 1024;
+    constexpr int SLOT_BYTES = ROW_BYTES + kMetaBytes;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    RingHeader* hdr = reinterpret_cast<RingHeader*>(smem);
+    char* ring = smem + sizeof(RingHeader);
+
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int chain = blockIdx.x;
+    const ChainDesc dsc = L.descs[chain];
+    const int d = kp.d;
+    const int64_t n = dsc.n_rows;
+    const int R = ring_rows;
+
+    if (threadIdx.x == 0) {
+        hdr->ready = 0;
+        hdr->consumed = 0;
+        hdr->stop = 0;
+    }
+    __syncthreads();
+
+    if (wave == 1) {
+        // ---------------- loader ----------------
+        constexpr int D = loader_depth<NV>();
+        const S* X = reinterpret_cast<const S*>(dsc.x);
+        const int64_t ld = dsc.ld;
+        // meta: lanes 0/1 -> label lo/hi, 2/3 -> step lo/hi (other lanes duplicate)
+        const unsigned* ysrc = reinterpret_cast<const unsigned*>((lane & 2) ? L.steps : dsc.y) + (lane & 1);
+        unsigned consumed = 0;
+        int slot = 0;
+        for (int64_t t = 0; t < n; ++t) {
+            if (t >= (int64_t)consumed + R) {
+                // wait for the compute wave to free the slot of row t - R
+                for (;;) {
+                    consumed = lds_load_u32_asm(&hdr->consumed);
+                    if (t < (int64_t)consumed + R) break;
+                    if (lds_load_u32_asm(&hdr->stop)) goto drain;
+                    __builtin_amdgcn_s_sleep(2);
+                }
+            }
+            {
+                char* dst = ring + slot * SLOT_BYTES;
+                const V* row = reinterpret_cast<const V*>(X + t * ld);
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    if (FULL || (v * 64 + lane) * VEC < ld)
+                        __builtin_amdgcn_global_load_lds(
+                            (const void*)(as_global(row + v * 64 + lane)),
+                            (__attribute__((address_space(3))) void*)(dst + v * 1024), 16, 0, 0);
+                }
+                __builtin_amdgcn_global_load_lds((const void*)(as_global(ysrc + 2 * t)),
+                                                 (__attribute__((address_space(3))) void*)(dst + ROW_BYTES),
+                                                 4, 0, 0);
+            }
+            if (++slot == R) slot = 0;
+            if (t >= D) {
+                // the oldest of the D rows in flight (row t - D) has landed
+                asm volatile("s_waitcnt vmcnt(%0)" : : "n"(D * (NV + 1)) : "memory");
+                lds_store_u32_asm(&hdr->ready, (unsigned)(t - D + 1));
+            }
+        }
+    drain:
+        asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
+        lds_store_u32_asm(&hdr->ready, (unsigned)n);
+        return;
+    }
+
+    // ---------------- compute ----------------
+    T w[E];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const int base = (v * 64 + lane) * VEC;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            const int f = base + k;
+            const double wv = as_global(L.w_in)[f < d ? f : 0];  // unconditional, clamped
+            w[v * VEC + k] = f < d ? T(wv) : T(0);
+        }
+    }
+
+    double loss_sum = 0.0;
+    int64_t count = 0;
+    unsigned ready = 0;
+    int slot = 0;
+    for (int64_t t = 0; t < n; ++t) {
+        if (t >= (int64_t)ready) {
+            for (;;) {
+                ready = __hip_atomic_load(&hdr->ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (t < (int64_t)ready) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        const char* src = ring + slot * SLOT_BYTES;
+        T x[E];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            const V xv = *reinterpret_cast<const V*>(src + v * 1024 + lane * 16);
+            unpack<S, T>(xv, x + v * VEC);
+        }
+        const f64x2 meta = *reinterpret_cast<const f64x2*>(src + ROW_BYTES);
+        const T y = T(meta.x);
+        const T s = T(meta.y);
+        if (++slot == R) slot = 0;
+
+        // dot(data, weights)
+        T acc0 = T(0), acc1 = T(0);
+#pragma unroll
+        for (int e = 0; e < E; e += 2) {
+            acc0 = m_fma(x[e], w[e], acc0);
+            if (e + 1 < E) acc1 = m_fma(x[e + 1], w[e + 1], acc1);
+        }
+        // the slot has been read (x feeds the FMAs above): hand it back to the loader
+        __hip_atomic_store(&hdr->consumed, (unsigned)(t + 1), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+        const T z = wave_sum(acc0 + acc1);
+
+        T mult;
+        const T loss = gradient_scalar<GRAD, T>(z, y, mult);
+        loss_sum += double(loss);
+        count += 1;
+
+        const T a = -s;
+        T dsq = T(0), nsq = T(0);
+        if constexpr (UPD == U_SQUARED_L2) {
+            const T c = T(1) - s * T(kp.reg);
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const T old = w[e];
+                T nw = old * c;
+                nw = nw + a * (mult * x[e]);
+                w[e] = nw;
+                if constexpr (CONV) { const T df = old - nw; dsq += df * df; nsq += nw * nw; }
+            }
+        } else if constexpr (UPD == U_L1) {
+            const T shrink = T(kp.reg) * s;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const T old = w[e];
+                T nw = old + a * (mult * x[e]);
+                nw = jsignum(nw) * jmax(T(0), m_fabs(nw) - shrink);
+                w[e] = nw;
+                if constexpr (CONV) { const T df = old - nw; dsq += df * df; nsq += nw * nw; }
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const T old = w[e];
+                const T nw = old + a * (mult * x[e]);
+                w[e] = nw;
+                if constexpr (CONV) { const T df = old - nw; dsq += df * df; nsq += nw * nw; }
+            }
+        }
+        if constexpr (CONV) {
+            wave_sum2(dsq, nsq);
+            // ||old - new|| < tol * max(||new||, 1.0)   (PSGD.scala:262, :333-335)
+            if (m_sqrt(dsq) < T(kp.tol) * jmax(m_sqrt(nsq), T(1))) {
+                __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                break;
+            }
+        }
+    }
+
+    // regVal of the chain's last update (PSGD.scala:257; 0.0 if no sample, :247)
+    double rv = 0.0;
+    if constexpr (UPD == U_SQUARED_L2 || UPD == U_L1) {
+        T acc = T(0);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            if constexpr (UPD == U_SQUARED_L2) acc += w[e] * w[e];
+            else acc += m_fabs(w[e]);
+        }
+        acc = wave_sum(acc);
+        if (count > 0) {
+            if constexpr (UPD == U_SQUARED_L2) {
+                const double nrm = sqrt(double(acc));
+                rv = 0.5 * kp.reg * nrm * nrm;
+            } else {
+                rv = double(acc) * kp.reg;
+            }
+        }
+    }
+
+    double* wo = L.w_out + (int64_t)chain * d;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const int base = (v * 64 + lane) * VEC;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k)
+            if (base + k < d) wo[base + k] = double(w[v * VEC + k]);
+    }
+    if (lane == 0) {
+        L.rv[chain] = rv;
+        L.loss[chain] = loss_sum;
+        L.cnt[chain] = count;
+        L.cnt_d[chain] = double(count);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// chain_general: any d, dense or CSR rows, every updater. Parity path, fp64 compute.
+// The chain's working weights live in its own slice of w_out (global memory, L2-resident for
+// moderate d); stateful updaters keep their status in `state`. One wave per chain.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void wave_mem_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+}
+
+template <typename S, int LAYOUT, int GRAD, int UPD, bool CONV>
+__global__ __launch_bounds__(64) void chain_general(ChainLaunch L, KParams kp) {
+    const int lane = threadIdx.x;
+    const int chain = blockIdx.x;
+    const ChainDesc dsc = L.descs[chain];
+    const int d = kp.d;
+    const int64_t n = dsc.n_rows;
+    const gptr<S> X = as_global(reinterpret_cast<const S*>(dsc.x));
+    const gptr<double> Y = as_global(dsc.y);
+    const gptr<double> STEPS = as_global(L.steps);
+    const gptr<int64_t> ROWP = as_global(dsc.row_ptr);
+    const gptr<int32_t> COL = as_global(dsc.col);
+    const gmut<double> W = as_global_mut(L.w_out + (int64_t)chain * d);
+    const gmut<double> SA = L.state ? as_global_mut(L.state + (int64_t)chain * 2 * d) : nullptr;
+    const gmut<double> SB = L.state ? SA + d : nullptr;
+
+    for (int i = lane; i < d; i += 64) W[i] = as_global(L.w_in)[i];
+    wave_mem_fence();
+
+    double loss_sum = 0.0;
+    int64_t count = 0;
+    double rv = 0.0;
+    for (int64_t t = 0; t < n; ++t) {
+        const double y = Y[t];
+        const double s = STEPS[t];           // stepSize / math.sqrt(iter), iter = t + 1
+        gptr<S> xr = nullptr;
+        int64_t kb = 0, ke = 0;
+        // dot(data, weights)
+        double acc = 0.0;
+        if constexpr (LAYOUT == kDense) {
+            xr = X + t * dsc.ld;
+            for (int i = lane; i < d; i += 64) acc = m_fma(double(xr[i]), W[i], acc);
+        } else {
+            kb = ROWP[t];
+            ke = ROWP[t + 1];
+            for (int64_t k = kb + lane; k < ke; k += 64)
+                acc = m_fma(double(X[k]), W[COL[k]], acc);
+        }
+        const double z = wave_sum(acc);
+        double mult;
+        const double loss = gradient_scalar<GRAD, double>(z, y, mult);
+        loss_sum += loss;
+        count += 1;
+        const double a = -s;
+        double dsq = 0.0, nsq = 0.0;
+
+        if constexpr (UPD == U_SIMPLE && LAYOUT == kCsr) {
+            // Breeze axpy over the gradient's active entries only.
+            for (int64_t k = kb + lane; k < ke; k += 64) {
+                const int i = COL[k];
+                const double old = W[i];
+                const double nw = old + a * (mult * double(X[k]));
+                W[i] = nw;
+                if constexpr (CONV) { const double df = old - nw; dsq += df * df; }
+            }
+            if constexpr (CONV) {
+                wave_mem_fence();
+                for (int i = lane; i < d; i += 64) nsq += W[i] * W[i];
+            }
+        } else {
+            if constexpr (LAYOUT == kCsr) {
+                // Updaters that touch every coordinate: run the elementwise part over all d,
+                // with the gradient applied at the row's indices in a second pass (ordered as
+                // the reference: L2 scales before the axpy, L1 thresholds after it).
+                if constexpr (UPD == U_SQUARED_L2) {
+                    const double c = 1.0 - s * kp.reg;
+                    for (int i = lane; i < d; i += 64) {
+                        const double old = W[i];
+                        const double nw = old * c;
+                        W[i] = nw;
+                        if constexpr (CONV) SB[i] = old;   // keep old for the convergence test
+                    }
+                    wave_mem_fence();
+                    for (int64_t k = kb + lane; k < ke; k += 64) {
+                        const int i = COL[k];
+                        W[i] = W[i] + a * (mult * double(X[k]));
+                    }
+                } else if constexpr (UPD == U_L1) {
+                    if constexpr (CONV)
+                        for (int i = lane; i < d; i += 64) SB[i] = W[i];
+                    wave_mem_fence();
+                    for (int64_t k = kb + lane; k < ke; k += 64) {
+                        const int i = COL[k];
+                        W[i] = W[i] + a * (mult * double(X[k]));
+                    }
+                    wave_mem_fence();
+                    const double shrink = kp.reg * s;
+                    for (int i = lane; i < d; i += 64) {
+                        const double v = W[i];
+                        W[i] = jsignum(v) * jmax(0.0, fabs(v) - shrink);
+                    }
+                } else {
+                    static_assert(UPD == U_SQUARED_L2 || UPD == U_L1,
+                                  "CSR rows with a stateful updater are not built (EUNSUPPORTED)");
+                }
+                if constexpr (CONV && (UPD == U_SQUARED_L2 || UPD == U_L1)) {
+                    wave_mem_fence();
+                    for (int i = lane; i < d; i += 64) {
+                        const double nw = W[i];
+                        const double df = SB[i] - nw;
+                        dsq += df * df;
+                        nsq += nw * nw;
+                    }
+                }
+            } else {
+                if constexpr (UPD == U_SIMPLE) {
+                    for (int i = lane; i < d; i += 64) {
+                        const double old = W[i];
+                        const double nw = old + a * (mult * double(xr[i]));
+                        W[i] = nw;
+                        if constexpr (CONV) { const double df = old - nw; dsq += df * df; nsq += nw * nw; }
+                    }
+                } else if constexpr (UPD == U_SQUARED_L2) {
+                    const double c = 1.0 - s * kp.reg;
+                    for (int i = lane; i < d; i += 64) {
+                        const double old = W[i];
+                        double nw = old * c;
+                        nw = nw + a * (mult * double(xr[i]));
+                        W[i] = nw;
+                        if constexpr (CONV) { const double df = old - nw; dsq += df * df; nsq += nw * nw; }
+                    }
+                } else if constexpr (UPD == U_L1) {
+                    const double shrink = kp.reg * s;
+                    for (int i = lane; i < d; i += 64) {
+                        const double old = W[i];
+                        double nw = old + a * (mult * double(xr[i]));
+                        nw = jsignum(nw) * jmax(0.0, fabs(nw) - shrink);
+                        W[i] = nw;
+                        if constexpr (CONV) { const double df = old - nw; dsq += df * df; nsq += nw * nw; }
+                    }
+                } else if constexpr (UPD == U_ADAGRAD) {
+                    // accum = (first ? g*g : accum + g*g); w += -s * (g / sqrt(accum + 1.0))
+                    const bool first = (t == 0);
+                    for (int i = lane; i < d; i += 64) {
+                        const double g = mult * double(xr[i]);
+                        const double sq = g * g;
+                        const double acc2 = first ? sq : SA[i] + sq;
+                        SA[i] = acc2;
+                        const double old = W[i];
+                        const double nw = old + a * (g / sqrt(acc2 + 1.0));
+                        W[i] = nw;
+                        if constexpr (CONV) { const double df = old - nw; dsq += df * df; nsq += nw * nw; }
+                    }
+                } else {  // U_ADAM, UPD.scala:252-285 (reproduced literally)
+                    const bool first = (t == 0);
+                    const double beta = kp.beta, gamma = kp.gamma;
+                    const double iter = double(t + 1);
+                    const double lr = s / (1.0 - pow(beta, iter));
+                    const double al = -lr;
+                    for (int i = lane; i < d; i += 64) {
+                        const double g = mult * double(xr[i]);
+                        const double sq = g * g;
+                        double v, r;
+                        if (first) { v = g * (1 - beta); r = sq * (1 - gamma); }
+                        else { v = SA[i] * beta + g * (1 - beta); r = SB[i] * gamma + sq * (1 - gamma); }
+                        SA[i] = v;
+                        SB[i] = r;
+                        const double fix1 = sqrt(1.0 - pow(r, iter)) + kp.eps;
+                        const double old = W[i];
+                        const double nw = old + al * (v / fix1);
+                        W[i] = nw;
+                        if constexpr (CONV) { const double df = old - nw; dsq += df * df; nsq += nw * nw; }
+                    }
+                }
+            }
+        }
+        wave_mem_fence();
+        if constexpr (CONV) {
+            wave_sum2(dsq, nsq);
+            if (sqrt(dsq) < kp.tol * jmax(sqrt(nsq), 1.0)) break;
+        }
+    }
+
+    if constexpr (UPD == U_SQUARED_L2 || UPD == U_L1) {
+        double acc = 0.0;
+        for (int i = lane; i < d; i += 64) acc += (UPD == U_SQUARED_L2) ? W[i] * W[i] : fabs(W[i]);
+        acc = wave_sum(acc);
+        if (count > 0) {
+            if constexpr (UPD == U_SQUARED_L2) {
+                const double nrm = sqrt(acc);
+                rv = 0.5 * kp.reg * nrm * nrm;
+            } else {
+                rv = acc * kp.reg;
+            }
+        }
+    }
+    if (lane == 0) {
+        L.rv[chain] = rv;
+        L.loss[chain] = loss_sum;
+        L.cnt[chain] = count;
+        L.cnt_d[chain] = double(count);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// fold_kernel: the reference combiner (PSGD.scala:271-276) as a left fold over n items in
+// index order, one thread per coordinate; the thread with i == d folds the scalars.
+//   w = (w1*c1 + w2*c2) / (c1 + c2);  rv likewise;  loss = l1 + l2;  c = c1 + c2
+// out[0..d) = w, out[d] = regVal, out[d+1] = lossSum, out[d+2] = count.
+// ------------------------------------------------------------------------------------------
+__global__ void fold_kernel(const double* __restrict__ w, int64_t w_stride,
+                            const double* __restrict__ rv, const double* __restrict__ loss,
+                            const double* __restrict__ cnt, int64_t s_stride, int n, int d,
+                            double* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < d) {
+        double acc = w[i];
+        double c1 = cnt[0];
+        for (int p = 1; p < n; ++p) {
+            const double c2 = cnt[p * s_stride];
+            acc = (acc * c1 + w[p * w_stride + i] * c2) / (c1 + c2);
+            c1 = c1 + c2;
+        }
+        out[i] = acc;
+    } else if (i == d) {
+        double r = rv[0], l = loss[0], c1 = cnt[0];
+        for (int p = 1; p < n; ++p) {
+            const double c2 = cnt[p * s_stride];
+            r = (r * c1 + rv[p * s_stride] * c2) / (c1 + c2);
+            l = l + loss[p * s_stride];
+            c1 = c1 + c2;
+        }
+        out[d] = r;
+        out[d + 1] = l;
+        out[d + 2] = c1;
+    }
+}
+
+// sum((a-b)^2) and sum(b^2) (a may be null: then sum(b^2) and sum(|b|)) -- one block, fixed
+// reduction tree, deterministic.
+__global__ __launch_bounds__(256) void sq_terms_kernel(const double* __restrict__ a,
+                                                       const double* __restrict__ b, int d,
+                                                       double* __restrict__ out) {
+    __shared__ double s0[256], s1[256];
+    double t0 = 0.0, t1 = 0.0;
+    for (int i = threadIdx.x; i < d; i += 256) {
+        const double bv = b[i];
+        if (a) { const double df = a[i] - bv; t0 += df * df; t1 += bv * bv; }
+        else { t0 += bv * bv; t1 += fabs(bv); }
+    }
+    s0[threadIdx.x] = t0;
+    s1[threadIdx.x] = t1;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if (threadIdx.x < h) {
+            s0[threadIdx.x] += s0[threadIdx.x + h];
+            s1[threadIdx.x] += s1[threadIdx.x + h];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) { out[0] = s0[0]; out[1] = s1[0]; }
+}
+
+// stepSize / math.sqrt(iter) for iter = 1..n (SGDUpdater.scala:93, :133, :174, :210, :261).
+__global__ void steps_kernel(double step, int64_t n, double* __restrict__ steps) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) steps[j] = step / sqrt(double(j + 1));
+}
+
+// ------------------------------------------------------------------------------------------
+// Launchers / dispatch.
+// ------------------------------------------------------------------------------------------
+template <typename S, typename T, int GRAD, int UPD, bool CONV, int NV>
+static int launch_reg(const ChainLaunch& L, const KParams& kp, bool full, size_t lds, hipStream_t st) {
+    // LDS ring: header + R slots of (row + meta). `lds` is the per-workgroup budget chosen by
+    // the host (it also spreads the chains over the CUs).
+    constexpr int SLOT = NV * 1024 + kMetaBytes;
+    size_t budget = lds > 0 ? lds : (size_t)64 * 1024;
+    int rows = (int)((budget - sizeof(RingHeader)) / SLOT);
+    if (rows < 2) rows = 2;
+    const size_t bytes = sizeof(RingHeader) + (size_t)rows * SLOT;
+    if (full) {
+        auto k = chain_dense<S, T, GRAD, UPD, CONV, NV, true>;
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(128), bytes, st, L, kp, rows);
+    } else {
+        auto k = chain_dense<S, T, GRAD, UPD, CONV, NV, false>;
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(128), bytes, st, L, kp, rows);
+    }
+    return (int)hipGetLastError();
+}
+
+template <typename S, typename T, int GRAD, int UPD, bool CONV>
+static int dispatch_nv(const ChainLaunch& L, const KParams& kp, int64_t min_ld, int64_t max_ld,
+                       size_t lds, hipStream_t st, int* variant) {
+    constexpr int VEC = 16 / sizeof(S);
+    int nv = 1;
+    while (nv * 64 * VEC < max_ld) nv *= 2;
+    // FULL: every lane's every vector is inside every row (no exec masking on the loads).
+    const bool full = min_ld >= (int64_t)nv * 64 * VEC;
+    if (variant) *variant = 100 + nv;
+    switch (nv) {
+    case 1: return launch_reg<S, T, GRAD, UPD, CONV, 1>(L, kp, full, lds, st);
+    case 2: return launch_reg<S, T, GRAD, UPD, CONV, 2>(L, kp, full, lds, st);
+    case 4: return launch_reg<S, T, GRAD, UPD, CONV, 4>(L, kp, full, lds, st);
+    case 8: return launch_reg<S, T, GRAD, UPD, CONV, 8>(L, kp, full, lds, st);
+    default: return -1;
+    }
+}
+
+template <typename S, int LAYOUT, int GRAD, int UPD, bool CONV>
+static int launch_gen(const ChainLaunch& L, const KParams& kp, hipStream_t st, int* variant) {
+    if (variant) *variant = 200 + LAYOUT;
+    hipLaunchKernelGGL((chain_general<S, LAYOUT, GRAD, UPD, CONV>), dim3(kp.n_chains), dim3(64), 0,
+                       st, L, kp);
+    return (int)hipGetLastError();
+}
+
+template <typename S, int GRAD, int UPD, bool CONV>
+static int dispatch_layout(const ChainLaunch& L, const KParams& kp, int layout, int compute,
+                           int64_t min_ld, int64_t max_ld, size_t lds, hipStream_t st, int* variant) {
+    constexpr int VEC = 16 / sizeof(S);
+    if constexpr (UPD <= U_L1) {
+        if (layout == kDense && max_ld <= 8 * 64 * VEC) {
+            if (compute == 1) return dispatch_nv<S, float, GRAD, UPD, CONV>(L, kp, min_ld, max_ld, lds, st, variant);
+            return dispatch_nv<S, double, GRAD, UPD, CONV>(L, kp, min_ld, max_ld, lds, st, variant);
+        }
+    }
+    if (layout == kDense) return launch_gen<S, kDense, GRAD, UPD, CONV>(L, kp, st, variant);
+    if constexpr (UPD == U_ADAGRAD || UPD == U_ADAM) return -2;  // CSR + stateful: not built
+    else return launch_gen<S, kCsr, GRAD, UPD, CONV>(L, kp, st, variant);
+}
+
+template <typename S, int GRAD, int UPD>
+static int dispatch_conv(const ChainLaunch& L, const KParams& kp, int layout, int compute,
+                         bool conv, int64_t min_ld, int64_t max_ld, size_t lds, hipStream_t st, int* variant) {
+    if (conv) return dispatch_layout<S, GRAD, UPD, true>(L, kp, layout, compute, min_ld, max_ld, lds, st, variant);
+    return dispatch_layout<S, GRAD, UPD, false>(L, kp, layout, compute, min_ld, max_ld, lds, st, variant);
+}
+
+template <typename S, int GRAD>
+static int dispatch_upd(const ChainLaunch& L, const KParams& kp, int layout, int compute, int upd,
+                        bool conv, int64_t min_ld, int64_t max_ld, size_t lds, hipStream_t st, int* variant) {
+    switch (upd) {
+    case U_SIMPLE: return dispatch_conv<S, GRAD, U_SIMPLE>(L, kp, layout, compute, conv, min_ld, max_ld, lds, st, variant);
+    case U_SQUARED_L2: return dispatch_conv<S, GRAD, U_SQUARED_L2>(L, kp, layout, compute, conv, min_ld, max_ld, lds, st, variant);
+    case U_L1: return dispatch_conv<S, GRAD, U_L1>(L, kp, layout, compute, conv, min_ld, max_ld, lds, st, variant);
+    case U_ADAGRAD: return dispatch_conv<S, GRAD, U_ADAGRAD>(L, kp, layout, compute, conv, min_ld, max_ld, lds, st, variant);
+    case U_ADAM: return dispatch_conv<S, GRAD, U_ADAM>(L, kp, layout, compute, conv, min_ld, max_ld, lds, st, variant);
+    default: return -1;
+    }
+}
+
+template <typename S>
+static int dispatch_grad(const ChainLaunch& L, const KParams& kp, int layout, int compute, int grad,
+                         int upd, bool conv, int64_t min_ld, int64_t max_ld, size_t lds,
+                         hipStream_t st, int* variant) {
+    switch (grad) {
+    case G_LOGISTIC: return dispatch_upd<S, G_LOGISTIC>(L, kp, layout, compute, upd, conv, min_ld, max_ld, lds, st, variant);
+    case G_LEAST_SQUARES: return dispatch_upd<S, G_LEAST_SQUARES>(L, kp, layout, compute, upd, conv, min_ld, max_ld, lds, st, variant);
+    case G_HINGE: return dispatch_upd<S, G_HINGE>(L, kp, layout, compute, upd, conv, min_ld, max_ld, lds, st, variant);
+    default: return -1;
+    }
+}
+
+int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int storage, int compute,
+                  int gradient, int updater, bool check_conv, int64_t min_ld, int64_t max_ld,
+                  int lds_spread, hipStream_t stream, int* kernel_variant) {
+    if (kp.n_chains <= 0) return 0;
+    const size_t lds = (size_t)(lds_spread > 0 ? lds_spread : 0);
+    if (storage == 1)
+        return dispatch_grad<float>(L, kp, layout, compute, gradient, updater, check_conv, min_ld,
+                                    max_ld, lds, stream, kernel_variant);
+    return dispatch_grad<double>(L, kp, layout, compute, gradient, updater, check_conv, min_ld,
+                                 max_ld, lds, stream, kernel_variant);
+}
+
+int launch_fold(const double* w, int64_t w_stride, const double* rv, const double* loss,
+                const double* cnt, int64_t s_stride, int n, int d, double* out,
+                hipStream_t stream) {
+    if (n <= 0) return -1;
+    const int threads = 256;
+    const int blocks = (d + 1 + threads - 1) / threads;
+    hipLaunchKernelGGL(fold_kernel, dim3(blocks), dim3(threads), 0, stream, w, w_stride, rv, loss,
+                       cnt, s_stride, n, d, out);
+    return (int)hipGetLastError();
+}
+
+int launch_sq_terms(const double* a, const double* b, int d, double* out2, hipStream_t stream) {
+    hipLaunchKernelGGL(sq_terms_kernel, dim3(1), dim3(256), 0, stream, a, b, d, out2);
+    return (int)hipGetLastError();
+}
+
+int launch_steps(double step, int64_t n, double* steps, hipStream_t stream) {
+    if (n <= 0) return 0;
+    const int threads = 256;
+    const int64_t blocks = (n + threads - 1) / threads;
+    hipLaunchKernelGGL(steps_kernel, dim3((unsigned)blocks), dim3(threads), 0, stream, step, n, steps);
+    return (int)hipGetLastError();
+}
+
+}  // namespace psgd

@@ -1,0 +1,329 @@
+"""ParallelizedSGD -- the reference's Optimizer API and driver loop, with the per-partition
+chains, the per-sample Gradient/SGDUpdater math and the model averaging on MI355X.
+
+Reference: src/main/scala/org/apache/spark/mllib/optimization/ParallelizedSGD.scala
+  class ParallelizedSGD(gradient, updater)  :41-159   -> class ParallelizedSGD below
+  object ParallelizedSGD.runParallelizedSGD :188-306  -> ParallelizedSGD.runParallelizedSGD
+  8-argument alias (tol 0.001)              :311-321  -> the default of convergenceTol
+  isConverged                               :324-336  -> device terms + the comparison here
+
+What runs where: the driver loop below is the reference's, statement for statement (loss
+history, regVal lag, driver-side convergence test, empty-data and empty-batch rules). The block
+the reference ships to executors (:238-276: broadcast, sample, mapPartitions chain, treeReduce)
+is one psgd_run_epoch_device call per process (HIP chain kernel + on-device fold in partition
+order), then -- with several processes -- an all-gather of the per-process partial results over
+RCCL and the same fold in rank order (the cross-GPU level of the treeReduce).
+"""
+from __future__ import annotations
+
+import logging
+import math
+import uuid
+from typing import List, Optional, Tuple
+
+import numpy as np
+
+from . import _native as N
+from .data import CsrPartition, DensePartition, DevicePartition, PartitionedData, shard_range
+from .gradient import Gradient, gradient_kind
+from .updater import AdamSGDUpdater, SGDUpdater, updater_kind
+
+log = logging.getLogger("org.apache.spark.mllib.optimization.ParallelizedSGD")
+
+IllegalArgumentException = N.IllegalArgumentException
+
+
+def _require(cond: bool, msg: str) -> None:
+    if not cond:
+        raise IllegalArgumentException("requirement failed: " + msg)
+
+
+def _jstr(x) -> str:
+    """Scala string interpolation of a Double/Int."""
+    if isinstance(x, float):
+        return repr(x) if math.isfinite(x) else ("NaN" if x != x else ("Infinity" if x > 0 else "-Infinity"))
+    return str(x)
+
+
+def make_params(gradient, updater, stepSize, regParam, miniBatchFraction, convergenceTol,
+                compute_dtype="f64", iteration=1) -> N.psgd_params:
+    p = N.psgd_params()
+    p.gradient = gradient_kind(gradient)
+    p.updater = updater_kind(updater)
+    p.compute_dtype = {"f64": N.F64, "f32": N.F32}[compute_dtype]
+    p.iteration = iteration
+    p.step_size = float(stepSize)
+    p.reg_param = float(regParam)
+    p.mini_batch_fraction = float(miniBatchFraction)
+    p.convergence_tol = float(convergenceTol)
+    if isinstance(updater, AdamSGDUpdater):
+        p.adam_beta, p.adam_gamma, p.adam_eps = updater.beta, updater.gamma, updater.eps
+    else:
+        p.adam_beta, p.adam_gamma, p.adam_eps = 0.9, 0.999, 1e-8
+    return p
+
+
+def _dist():
+    """(rank, world, process_group_available) from torch.distributed, if initialised."""
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_rank(), dist.get_world_size(), True
+    except ImportError:
+        pass
+    return 0, 1, False
+
+
+# ---------------------------------------------------------------------------------------------
+# HIP engine: device-resident weights, one psgd_ctx per process.
+# ---------------------------------------------------------------------------------------------
+_contexts = {}
+
+
+def get_context(device: int) -> N.Context:
+    ctx = _contexts.get(device)
+    if ctx is None:
+        ctx = N.Context(device)
+        ctx.registered_token = None
+        _contexts[device] = ctx
+    return ctx
+
+
+class HipEngine:
+    """Runs the chains of this process's partitions on one MI355X (psgd C ABI).
+
+    Weights and the (d+3)-double partial results stay in HBM (torch tensors used only as
+    device allocations and as the RCCL all-gather buffers)."""
+
+    def __init__(self, data: PartitionedData, rank: int = 0, world: int = 1,
+                 device: Optional[int] = None):
+        import torch
+        if not torch.cuda.is_available():
+            raise N.DeviceError("HipEngine needs a visible MI355X (torch.cuda.is_available() is False)")
+        if device is None:
+            device = torch.cuda.current_device()
+        self.torch = torch
+        self.device = device
+        self.dev = torch.device("cuda", device)
+        self.ctx = get_context(device)
+        self.d = data.num_features
+        self.rank, self.world = rank, world
+        self.lo, self.hi = shard_range(data.num_partitions, rank, world)
+        self._register(data)
+
+    def _register(self, data: PartitionedData):
+        token = getattr(data, "_psgd_token", None)
+        if token is None:
+            token = uuid.uuid4().hex
+            data._psgd_token = token
+        key = (token, self.lo, self.hi)
+        if self.ctx.registered_token == key:
+            return
+        self.ctx.clear()
+        for p in range(self.lo, self.hi):
+            part = data.partitions[p]
+            if isinstance(part, DensePartition):
+                self.ctx.register_dense(p, part.labels, part.x)
+            elif isinstance(part, CsrPartition):
+                self.ctx.register_csr(p, part.labels, part.row_ptr, part.col, part.val, part.d)
+            elif isinstance(part, DevicePartition):
+                dt = N.F32 if part.x.dtype == self.torch.float32 else N.F64
+                self.ctx.register_dense_device(p, part.n_rows, part.d, int(part.x.stride(0)),
+                                               part.labels.data_ptr(), part.x.data_ptr(), dt)
+            else:
+                raise IllegalArgumentException(f"unsupported partition type {type(part).__name__}")
+        self.ctx.registered_token = key
+        self._partial = self.torch.empty(self.d + 3, dtype=self.torch.float64, device=self.dev)
+        self._gather = (self.torch.empty(self.world * (self.d + 3), dtype=self.torch.float64,
+                                         device=self.dev) if self.world > 1 else None)
+        self._folded = self.torch.empty(self.d + 3, dtype=self.torch.float64, device=self.dev)
+        self.n_local = self.hi - self.lo
+        self._counts = self.torch.empty(max(self.n_local, 1), dtype=self.torch.int64, device=self.dev)
+
+    # driver hooks ---------------------------------------------------------------------------
+    def weights(self, w_host: np.ndarray):
+        return self.torch.from_numpy(np.ascontiguousarray(w_host, dtype=np.float64)).to(self.dev)
+
+    def initial_regval(self, params, w_host: np.ndarray) -> float:
+        return self.ctx.initial_regval(params, w_host)
+
+    def epoch(self, params, w_dev, with_counts: bool = False):
+        """PSGD.scala:238-276 for all ranks: returns the folded (d+3) device vector
+        [w_avg, regVal, lossSum, count] and (optionally) this rank's chain counts."""
+        stream = self.torch.cuda.current_stream(self.dev).cuda_stream
+        if self.n_local > 0:
+            self.ctx.run_epoch_device(params, w_dev.data_ptr(), self._partial.data_ptr(),
+                                      self._counts.data_ptr() if with_counts else None, stream)
+        if self.world == 1:
+            out = self._partial
+        else:
+            import torch.distributed as dist
+            if self.n_local == 0:
+                # an empty rank contributes the identity of the fold: (w_in, 0, 0, 0)
+                self._partial[: self.d].copy_(w_dev)
+                self._partial[self.d:].zero_()
+            dist.all_gather_into_tensor(self._gather, self._partial)
+            self.ctx.fold_partials_device(self.world, self.d, self._gather.data_ptr(),
+                                          self._folded.data_ptr(), stream)
+            out = self._folded
+        counts = self._counts[: self.n_local].cpu().numpy() if with_counts else None
+        return out, counts
+
+    def scalars(self, folded) -> Tuple[float, float, int]:
+        h = folded[self.d:].cpu().numpy()
+        return float(h[0]), float(h[1]), int(h[2])
+
+    def adopt(self, folded):
+        return folded[: self.d].clone()
+
+    def convergence_terms(self, prev, cur) -> Tuple[float, float]:
+        stream = self.torch.cuda.current_stream(self.dev).cuda_stream
+        return self.ctx.convergence_terms_device(self.d, prev.data_ptr(), cur.data_ptr(), stream)
+
+    def to_host(self, w_dev) -> np.ndarray:
+        return w_dev.detach().cpu().numpy().astype(np.float64)
+
+
+# ---------------------------------------------------------------------------------------------
+# The optimizer.
+# ---------------------------------------------------------------------------------------------
+class ParallelizedSGD:
+    """:: Experimental :: Parallelized Stochastic Gradient Descent (Zinkevich et al.).
+
+    Mirrors ParallelizedSGD.scala:41-159: same defaults (:46-50), same validated setters
+    (:56-134, same messages), optimize(data, initialWeights) -> weights (:144-157)."""
+
+    def __init__(self, gradient: Gradient, updater: SGDUpdater):
+        self.gradient = gradient
+        self.updater = updater
+        self.stepSize = 1.0
+        self.numIterations = 100
+        self.regParam = 0.0
+        self.miniBatchFraction = 1.0
+        self.convergenceTol = 0.001
+        self.compute_dtype = "f64"
+
+    def setStepSize(self, step: float) -> "ParallelizedSGD":
+        _require(step > 0, f"Initial step size must be positive but got {_jstr(float(step))}")
+        self.stepSize = float(step)
+        return self
+
+    def setMiniBatchFraction(self, fraction: float) -> "ParallelizedSGD":
+        _require(fraction > 0 and fraction <= 1.0,
+                 f"Fraction for mini-batch SGD must be in range (0, 1] but got {_jstr(float(fraction))}")
+        self.miniBatchFraction = float(fraction)
+        return self
+
+    def setNumIterations(self, iters: int) -> "ParallelizedSGD":
+        _require(iters >= 0, f"Number of iterations must be nonnegative but got {iters}")
+        self.numIterations = int(iters)
+        return self
+
+    def setRegParam(self, regParam: float) -> "ParallelizedSGD":
+        _require(regParam >= 0,
+                 f"Regularization parameter must be nonnegative but got {_jstr(float(regParam))}")
+        self.regParam = float(regParam)
+        return self
+
+    def setConvergenceTol(self, tolerance: float) -> "ParallelizedSGD":
+        _require(tolerance >= 0.0 and tolerance <= 1.0,
+                 f"Convergence tolerance must be in range [0, 1] but got {_jstr(float(tolerance))}")
+        self.convergenceTol = float(tolerance)
+        return self
+
+    def setGradient(self, gradient: Gradient) -> "ParallelizedSGD":
+        self.gradient = gradient
+        return self
+
+    def setUpdater(self, updater: SGDUpdater) -> "ParallelizedSGD":
+        self.updater = updater
+        return self
+
+    def setComputeDtype(self, dtype: str) -> "ParallelizedSGD":
+        """Build extension: "f64" (reference arithmetic, default) or "f32" (throughput mode)."""
+        _require(dtype in ("f64", "f32"), f"compute dtype must be f64 or f32 but got {dtype}")
+        self.compute_dtype = dtype
+        return self
+
+    def optimize(self, data: PartitionedData, initialWeights) -> np.ndarray:
+        weights, _ = ParallelizedSGD.runParallelizedSGD(
+            data, self.gradient, self.updater, self.stepSize, self.numIterations, self.regParam,
+            self.miniBatchFraction, initialWeights, self.convergenceTol,
+            compute_dtype=self.compute_dtype)
+        return weights
+
+    # object ParallelizedSGD ---------------------------------------------------------------------
+    @staticmethod
+    def runParallelizedSGD(data: PartitionedData, gradient: Gradient, updater: SGDUpdater,
+                           stepSize: float, numIterations: int, regParam: float,
+                           miniBatchFraction: float, initialWeights, convergenceTol: float = 0.001,
+                           *, compute_dtype: str = "f64", engine=None,
+                           return_chain_counts: bool = False):
+        """ParallelizedSGD.scala:188-306 (and the 8-argument alias :311-321 via the default).
+        Returns (weights, stochasticLossHistory) [, per-iteration chain counts]."""
+        if miniBatchFraction < 1.0 and convergenceTol > 0.0:  # :200-203
+            log.warning("Testing against a convergenceTol when using miniBatchFraction "
+                        "< 1.0 can be unstable because of the stochasticity in sampling.")
+        history: List[float] = []
+        chain_counts: List[np.ndarray] = []
+        w0 = np.ascontiguousarray(np.asarray(initialWeights, dtype=np.float64))
+
+        numExamples = data.count()  # :211
+        if numExamples == 0:  # :214-217
+            log.warning("GradientDescent.runMiniBatchSGD returning initial weights, no data found")
+            out = (w0, np.array(history))
+            return out + (chain_counts,) if return_chain_counts else out
+        if numExamples * miniBatchFraction < 1:  # :219-221
+            log.warning("The miniBatchFraction is too small")
+        if w0.shape[0] != data.num_features:
+            raise IllegalArgumentException(
+                f"requirement failed: BLAS.dot(x: Vector, y: Vector) was given Vectors with "
+                f"non-matching sizes: x.size = {data.num_features}, y.size = {w0.shape[0]}")
+
+        if engine is None:
+            rank, world, _ = _dist()
+            engine = HipEngine(data, rank, world)
+
+        params = make_params(gradient, updater, stepSize, regParam, miniBatchFraction,
+                             convergenceTol, compute_dtype)
+        weights = engine.weights(w0)                      # :224
+        regVal = engine.initial_regval(params, w0)        # :231-233
+        have_current = False
+        converged = False
+        i = 1
+        while not converged and i <= numIterations:       # :237
+            params.iteration = i
+            folded, counts = engine.epoch(params, weights, with_counts=return_chain_counts)
+            avgRegVal, lossSum, batchSize = engine.scalars(folded)
+            if return_chain_counts:
+                chain_counts.append(counts)
+            if batchSize > 0:                              # :278
+                stochasticLoss = lossSum / batchSize + regVal   # :283
+                history.append(stochasticLoss)
+                log.warning("stochastic loss at step%d: %s", i, stochasticLoss)
+                new_weights = engine.adopt(folded)         # :286-287
+                regVal = avgRegVal
+                if have_current:                           # :289-294
+                    dsq, nsq = engine.convergence_terms(weights, new_weights)
+                    converged = math.sqrt(dsq) < convergenceTol * max_j(math.sqrt(nsq), 1.0)
+                weights = new_weights
+                have_current = True
+            else:                                          # :295-297
+                log.warning("Iteration (%d/%d). The size of sampled batch is zero", i, numIterations)
+            i += 1
+        log.info("GradientDescent.runMiniBatchSGD finished. Last 10 stochastic losses %s",
+                 ", ".join(str(v) for v in history[-10:]))
+        out = (engine.to_host(weights), np.array(history))
+        return out + (chain_counts,) if return_chain_counts else out
+
+
+def max_j(a: float, b: float) -> float:
+    """java.lang.Math.max (NaN-propagating)."""
+    if a != a:
+        return a
+    if b != b:
+        return b
+    return a if a >= b else b
+
+
+runParallelizedSGD = ParallelizedSGD.runParallelizedSGD

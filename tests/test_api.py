@@ -1,0 +1,134 @@
+"""Host-side API mirror of ParallelizedSGD.scala: setters, validation messages, partitioning,
+driver rules (with a scripted engine -- no device needed)."""
+import numpy as np
+import pytest
+
+
+def test_defaults_and_setters(pkg):
+    o = pkg.ParallelizedSGD(pkg.LogisticGradient(), pkg.SimpleSGDUpdater())
+    assert (o.stepSize, o.numIterations, o.regParam, o.miniBatchFraction, o.convergenceTol) == \
+        (1.0, 100, 0.0, 1.0, 0.001)
+    assert o.setStepSize(0.5).setNumIterations(3).setRegParam(0.1).setConvergenceTol(0.0) is o
+    assert (o.stepSize, o.numIterations, o.regParam, o.convergenceTol) == (0.5, 3, 0.1, 0.0)
+
+
+@pytest.mark.parametrize("call,msg", [
+    (lambda o: o.setStepSize(0.0), "requirement failed: Initial step size must be positive but got 0.0"),
+    (lambda o: o.setStepSize(-1), "requirement failed: Initial step size must be positive but got -1.0"),
+    (lambda o: o.setMiniBatchFraction(0.0),
+     "requirement failed: Fraction for mini-batch SGD must be in range (0, 1] but got 0.0"),
+    (lambda o: o.setMiniBatchFraction(1.5),
+     "requirement failed: Fraction for mini-batch SGD must be in range (0, 1] but got 1.5"),
+    (lambda o: o.setNumIterations(-1), "requirement failed: Number of iterations must be nonnegative but got -1"),
+    (lambda o: o.setRegParam(-0.5), "requirement failed: Regularization parameter must be nonnegative but got -0.5"),
+    (lambda o: o.setConvergenceTol(1.5),
+     "requirement failed: Convergence tolerance must be in range [0, 1] but got 1.5"),
+])
+def test_setter_validation_messages(pkg, call, msg):
+    o = pkg.ParallelizedSGD(pkg.LogisticGradient(), pkg.SimpleSGDUpdater())
+    with pytest.raises(pkg.IllegalArgumentException) as ei:
+        call(o)
+    assert str(ei.value) == msg
+
+
+def test_parallelize_slices_like_spark(pkg):
+    y = np.arange(10.0)
+    d = pkg.PartitionedData.parallelize(y, np.ones((10, 2)), 3)
+    assert [list(p.labels) for p in d.partitions] == [[0, 1, 2], [3, 4, 5], [6, 7, 8, 9]]
+    d = pkg.PartitionedData.parallelize(y[:2], np.ones((2, 2)), 4)
+    assert [p.n_rows for p in d.partitions] == [0, 1, 0, 1]
+    assert d.count() == 2
+
+
+def test_shard_ranges_cover_partitions(pkg):
+    for P in (1, 2, 5, 256, 2048):
+        for G in (1, 2, 3, 8):
+            spans = [pkg.shard_range(P, r, G) for r in range(G)]
+            assert spans[0][0] == 0 and spans[-1][1] == P
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(G - 1))
+            for r, (lo, hi) in enumerate(spans):
+                assert all(p * G // P == r for p in range(lo, hi))
+
+
+def test_csr_from_points(pkg):
+    pts = [(1.0, ([0, 3], [0.5, 1.0], 4)), (0.0, ([1], [2.0], 4)), (1.0, ([], [], 4))]
+    d = pkg.PartitionedData.from_points(pts, 2)
+    assert d.num_features == 4 and d.count() == 3
+    p0, p1 = d.partitions
+    assert list(p0.row_ptr) == [0, 2] and list(p1.row_ptr) == [0, 1, 1]
+
+
+def test_unsupported_plugins_raise(pkg):
+    class MyGradient(pkg.Gradient):
+        pass
+
+    with pytest.raises(pkg.IllegalArgumentException):
+        pkg.make_params(MyGradient(), pkg.SimpleSGDUpdater(), 1.0, 0.0, 1.0, 0.0)
+    with pytest.raises(pkg.UnsupportedOperationException):
+        pkg.LogisticGradient(numClasses=3)
+
+
+class ScriptedEngine:
+    """Returns canned fold results to exercise the driver's bookkeeping (PSGD.scala:237-299)."""
+
+    def __init__(self, results, d, terms=(1.0, 1.0), rv0=0.25):
+        self.results, self.d, self.terms, self.rv0, self.calls = list(results), d, terms, rv0, 0
+
+    def weights(self, w):
+        return np.array(w, dtype=float)
+
+    def initial_regval(self, params, w):
+        return self.rv0
+
+    def epoch(self, params, w, with_counts=False):
+        self.calls += 1
+        return self.results.pop(0), None
+
+    def scalars(self, f):
+        return f[self.d], f[self.d + 1], int(f[self.d + 2])
+
+    def adopt(self, f):
+        return np.array(f[: self.d])
+
+    def convergence_terms(self, prev, cur):
+        return self.terms
+
+    def to_host(self, w):
+        return np.array(w)
+
+
+def test_driver_regval_lag_and_empty_batch(pkg):
+    data = pkg.PartitionedData.parallelize(np.ones(4), np.ones((4, 2)), 2)
+    res = [np.array([1.0, 2.0, 0.5, 8.0, 4.0]),   # rv 0.5, lossSum 8, count 4
+           np.array([9.0, 9.0, 0.0, 0.0, 0.0]),   # empty batch: skipped
+           np.array([3.0, 4.0, 0.7, 2.0, 4.0])]
+    eng = ScriptedEngine(res, 2, terms=(100.0, 1.0))
+    w, h = pkg.runParallelizedSGD(data, pkg.LogisticGradient(), pkg.SquaredL2SGDUpdater(), 1.0, 3,
+                                  0.1, 1.0, [0.0, 0.0], 0.001, engine=eng)
+    # loss_i = lossSum/batch + regVal of the previous iteration (:283)
+    assert list(h) == [8.0 / 4 + 0.25, 2.0 / 4 + 0.5]
+    assert list(w) == [3.0, 4.0]
+
+
+def test_driver_convergence_from_second_success(pkg):
+    data = pkg.PartitionedData.parallelize(np.ones(4), np.ones((4, 2)), 2)
+    res = [np.array([1.0, 2.0, 0.0, 8.0, 4.0]) for _ in range(5)]
+    eng = ScriptedEngine(res, 2, terms=(0.0, 1.0))  # ||diff|| = 0 < tol -> converged
+    w, h = pkg.runParallelizedSGD(data, pkg.LogisticGradient(), pkg.SimpleSGDUpdater(), 1.0, 5,
+                                  0.0, 1.0, [0.0, 0.0], 0.001, engine=eng)
+    assert eng.calls == 2 and len(h) == 2
+
+
+def test_driver_empty_data_returns_initial_weights(pkg):
+    data = pkg.PartitionedData.parallelize(np.zeros(0), np.zeros((0, 3)), 2)
+    w, h = pkg.runParallelizedSGD(data, pkg.LogisticGradient(), pkg.SimpleSGDUpdater(), 1.0, 5,
+                                  0.0, 1.0, [1.0, 2.0, 3.0])
+    assert list(w) == [1.0, 2.0, 3.0] and len(h) == 0
+
+
+def test_driver_zero_iterations(pkg):
+    data = pkg.PartitionedData.parallelize(np.ones(4), np.ones((4, 2)), 2)
+    eng = ScriptedEngine([], 2)
+    w, h = pkg.runParallelizedSGD(data, pkg.LogisticGradient(), pkg.SimpleSGDUpdater(), 1.0, 0,
+                                  0.0, 1.0, [0.5, 0.5], engine=eng)
+    assert list(w) == [0.5, 0.5] and len(h) == 0 and eng.calls == 0

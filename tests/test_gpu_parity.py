@@ -1,0 +1,265 @@
+"""Parity of the HIP path (libpsgd.so through the C ABI) with the CPU oracle.
+
+fp64 mode: weights and loss history within 1e-9 relative (TestingUtils relTol semantics,
+TestingUtils.scala:34-46, with an absolute floor of 1e-12 near zero) and per-iteration chain
+counts EXACTLY equal (including the per-sample convergence breaks).
+fp32 storage + fp64 compute: the oracle runs on the same (fp32-representable) inputs: 1e-9.
+fp32 compute (throughput mode): stated tolerance FP32_REL below, versus the fp64 oracle.
+"""
+import numpy as np
+import pytest
+
+from conftest import has_gpu
+
+pytestmark = pytest.mark.gpu
+
+REL = 1e-9
+ABS_FLOOR = 1e-12
+FP32_REL = 2e-4       # weights, fp32 compute vs fp64 oracle
+FP32_LOSS_REL = 1e-4  # loss history
+
+
+def assert_close(a, b, rel=REL, floor=ABS_FLOOR, what=""):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    both_nan = np.isnan(a) & np.isnan(b)
+    diff = np.abs(a - b)
+    ok = both_nan | (diff <= rel * np.maximum(np.abs(a), np.abs(b))) | (diff <= floor)
+    if not ok.all():
+        i = int(np.argmax(~ok))
+        raise AssertionError(f"{what}: {int((~ok).sum())} mismatches; first at {i}: {a.flat[i]!r} vs "
+                             f"{b.flat[i]!r} (max rel {np.nanmax(diff / np.maximum(np.abs(b), 1e-300)):.3g})")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not has_gpu():
+        pytest.skip("no GPU")
+
+
+G = {"logistic": "LogisticGradient", "least_squares": "LeastSquaresGradient", "hinge": "HingeGradient"}
+U = {"simple": "SimpleSGDUpdater", "squared_l2": "SquaredL2SGDUpdater", "l1": "L1SGDUpdater",
+     "adagrad": "AdaGradSGDUpdater", "adam": "AdamSGDUpdater"}
+
+
+def data_for(pkg, oracle, case):
+    offs = case["offsets"]
+    P = len(offs) - 1
+    if case["source"] == "suite":
+        x, y = oracle.generate_gd_input(2.0, -1.5, case["n"], 42)
+        X = np.stack([np.ones(len(x)), x], 1) if case["bias_first"] else np.stack([x, np.ones(len(x))], 1)
+        assert [float(v) for v in X[: len(case["x_head"]), 1 if case["bias_first"] else 0]] == case["x_head"]
+        parts = [pkg.DensePartition(y[a:b], X[a:b]) for a, b in zip(offs[:-1], offs[1:])]
+    elif "X" in case:
+        X, y = np.array(case["X"]), np.array(case["y"])
+        parts = [pkg.DensePartition(y[a:b], X[a:b]) for a, b in zip(offs[:-1], offs[1:])]
+    else:
+        rp, col, val, y = (np.array(case["row_ptr"]), np.array(case["col"], np.int32),
+                           np.array(case["val"]), np.array(case["y"]))
+        parts = [pkg.CsrPartition(y[a:b], rp[a:b + 1] - rp[a], col[rp[a]:rp[b]], val[rp[a]:rp[b]], case["d"])
+                 for a, b in zip(offs[:-1], offs[1:])]
+    assert len(parts) == P
+    return pkg.PartitionedData(parts)
+
+
+def run_case(pkg, data, case, **kw):
+    g = getattr(pkg, G[case["gradient"]])()
+    u = getattr(pkg, U[case["updater"]])()
+    return pkg.runParallelizedSGD(data, g, u, case["step"], case["iters"], case["reg"], 1.0,
+                                  np.array(case["w0"]), case["tol"], return_chain_counts=True, **kw)
+
+
+def test_golden_cases_fp64(pkg, oracle, golden):
+    for case in golden:
+        data = data_for(pkg, oracle, case)
+        w, h, counts = run_case(pkg, data, case)
+        e = case["expected"]
+        assert [list(map(int, c)) for c in counts] == e["chain_counts"], case["name"]
+        assert_close(w, e["weights"], what=case["name"] + " weights")
+        assert_close(h, e["loss_history"], what=case["name"] + " loss")
+
+
+def test_suite_known_answers_on_gpu(pkg, oracle, golden):
+    """The reference suite's three assertions, re-run on the HIP path."""
+    by = {c["name"]: c for c in golden}
+    c = by["suite_loss_decreasing"]
+    _, h, _ = run_case(pkg, data_for(pkg, oracle, c), c)
+    assert h[-1] - h[0] < 0                                   # ParallelizedSGDSuite.scala:101
+    c0, c1 = by["suite_first_iteration_l2_reg0"], by["suite_first_iteration_l2_reg1"]
+    w0, l0, _ = run_case(pkg, data_for(pkg, oracle, c0), c0)
+    w1, l1, _ = run_case(pkg, data_for(pkg, oracle, c1), c1)
+    assert abs(l1[0] - (l0[0] + (1.0 + 0.25) / 2)) < 1e-5      # :132-135
+    assert abs(w1[0] - (w0[0] - 1.0)) < 1e-5 and abs(w1[1] - (w0[1] - 0.5)) < 1e-5  # :137-141
+    c = by["suite_convergence_tol"]
+    _, h, _ = run_case(pkg, data_for(pkg, oracle, c), c)
+    assert len(h) < 10                                        # :180
+
+
+def synth(rng, n, d, grad, dtype=np.float64):
+    X = rng.standard_normal((n, d)).astype(dtype)
+    wt = rng.standard_normal(d) / np.sqrt(d)
+    z = X.astype(np.float64) @ wt
+    if grad == "least_squares":
+        y = z + 0.1 * rng.standard_normal(n)
+    else:
+        y = ((z + rng.logistic(size=n)) > 0).astype(np.float64)
+    return X, y
+
+
+@pytest.mark.parametrize("d", [3, 100, 256, 300, 512, 700, 1024, 2048, 3000])
+@pytest.mark.parametrize("grad", ["logistic", "least_squares", "hinge"])
+def test_dense_fp64_sizes(pkg, oracle, d, grad):
+    rng = np.random.default_rng(d * 7 + len(grad))
+    n, P = 1200, 5
+    X, y = synth(rng, n, d, grad)
+    data = pkg.PartitionedData.parallelize(y, X, P)
+    offs = [i * n // P for i in range(P)] + [n]
+    step = 0.002 if grad == "least_squares" else 0.5
+    for upd in ("simple", "squared_l2", "l1"):
+        for tol in (0.0, 0.002):
+            w0 = 0.01 * np.ones(d)
+            w, h, c = pkg.runParallelizedSGD(data, getattr(pkg, G[grad])(), getattr(pkg, U[upd])(),
+                                             step, 3, 0.01, 1.0, w0, tol, return_chain_counts=True)
+            wr, hr, cr = oracle.run(oracle.Matrix(y, X), offs, grad, upd, step, 3, 0.01, w0, tol=tol,
+                                    n_threads=8)
+            tag = f"d={d} {grad} {upd} tol={tol}"
+            assert [list(x) for x in c] == [list(x) for x in cr[: len(c)]], tag
+            assert_close(w, wr, what=tag + " weights")
+            assert_close(h, hr, what=tag + " loss")
+
+
+@pytest.mark.parametrize("upd", ["adagrad", "adam"])
+def test_dense_stateful_updaters(pkg, oracle, upd):
+    rng = np.random.default_rng(11)
+    n, d, P = 600, 40, 3
+    X, y = synth(rng, n, d, "logistic")
+    data = pkg.PartitionedData.parallelize(y, X, P)
+    offs = [i * n // P for i in range(P)] + [n]
+    for tol in (0.0, 0.01):
+        w, h = pkg.runParallelizedSGD(data, pkg.LogisticGradient(), getattr(pkg, U[upd])(), 0.3, 3,
+                                      0.0, 1.0, np.zeros(d), tol)
+        wr, hr, _ = oracle.run(oracle.Matrix(y, X), offs, "logistic", upd, 0.3, 3, 0.0, np.zeros(d), tol=tol)
+        assert_close(w, wr, what=f"{upd} tol={tol}")
+        assert_close(h, hr, what=f"{upd} tol={tol} loss")
+
+
+def test_kernel_selection(pkg, oracle):
+    rng = np.random.default_rng(1)
+    for d, dtype, expect in ((100, np.float64, 101), (512, np.float32, 102), (1024, np.float32, 104),
+                             (3000, np.float64, 200)):
+        X, y = synth(rng, 64, d, "logistic", dtype)
+        data = pkg.PartitionedData.parallelize(y, X, 2, dtype=dtype)
+        pkg.runParallelizedSGD(data, pkg.LogisticGradient(), pkg.SimpleSGDUpdater(), 1.0, 1, 0.0, 1.0,
+                               np.zeros(d), 0.0)
+        ctx = pkg.optimization.get_context(0)
+        assert ctx.last_kernel() == expect, (d, dtype, ctx.last_kernel())
+
+
+def test_fp32_storage_fp64_compute(pkg, oracle):
+    rng = np.random.default_rng(5)
+    n, d, P = 4000, 512, 8
+    X, y = synth(rng, n, d, "least_squares", np.float32)
+    data = pkg.PartitionedData.parallelize(y, X, P, dtype=np.float32)
+    offs = [i * n // P for i in range(P)] + [n]
+    w, h = pkg.runParallelizedSGD(data, pkg.LeastSquaresGradient(), pkg.SimpleSGDUpdater(), 1e-3, 3,
+                                  0.0, 1.0, np.zeros(d), 0.0)
+    wr, hr, _ = oracle.run(oracle.Matrix(y, X.astype(np.float64)), offs, "least_squares", "simple",
+                           1e-3, 3, 0.0, np.zeros(d), tol=0.0, n_threads=8)
+    assert_close(w, wr, what="f32 storage weights")
+    assert_close(h, hr, what="f32 storage loss")
+
+
+@pytest.mark.parametrize("grad,d", [("least_squares", 512), ("logistic", 1024), ("hinge", 100)])
+def test_fp32_compute_mode_tolerance(pkg, oracle, grad, d):
+    rng = np.random.default_rng(9)
+    n, P = 20000, 4
+    X, y = synth(rng, n, d, grad, np.float32)
+    data = pkg.PartitionedData.parallelize(y, X, P, dtype=np.float32)
+    offs = [i * n // P for i in range(P)] + [n]
+    step = 1e-3 if grad == "least_squares" else 1.0
+    w, h = pkg.runParallelizedSGD(data, getattr(pkg, G[grad])(), pkg.SimpleSGDUpdater(), step, 3, 0.0,
+                                  1.0, np.zeros(d), 0.0, compute_dtype="f32")
+    wr, hr, _ = oracle.run(oracle.Matrix(y, X.astype(np.float64)), offs, grad, "simple", step, 3, 0.0,
+                           np.zeros(d), tol=0.0, n_threads=8)
+    scale = np.max(np.abs(wr))
+    assert np.max(np.abs(w - wr)) <= FP32_REL * scale, np.max(np.abs(w - wr)) / scale
+    assert_close(h, hr, rel=FP32_LOSS_REL, what="fp32 loss")
+
+
+def test_csr_stateful_updater_not_built(pkg):
+    data = pkg.PartitionedData.from_points([(1.0, ([0], [1.0], 3)), (0.0, ([2], [0.5], 3))], 1)
+    with pytest.raises(pkg.UnsupportedOperationException):
+        pkg.runParallelizedSGD(data, pkg.HingeGradient(), pkg.AdaGradSGDUpdater(), 1.0, 1, 0.0, 1.0,
+                               np.zeros(3), 0.0)
+
+
+def test_mini_batch_fraction(pkg):
+    rng = np.random.default_rng(2)
+    X, y = synth(rng, 100, 8, "logistic")
+    data = pkg.PartitionedData.parallelize(y, X, 2)
+    with pytest.raises(pkg.UnsupportedOperationException):
+        pkg.runParallelizedSGD(data, pkg.LogisticGradient(), pkg.SimpleSGDUpdater(), 1.0, 1, 0.0, 0.5,
+                               np.zeros(8), 0.0)
+
+
+def test_empty_partitions_nan_poisoning(pkg, oracle):
+    """Two leading empty partitions: (w*0 + w*0)/0 = NaN, as the reference's combiner gives when
+    Spark merges them first (ParallelizedSGD.scala:272-274)."""
+    X = np.array([[1.0, 2.0], [0.5, -1.0]])
+    y = np.array([1.0, 0.0])
+    parts = [pkg.DensePartition(y[:0], X[:0]), pkg.DensePartition(y[:0], X[:0]), pkg.DensePartition(y, X)]
+    w, h = pkg.runParallelizedSGD(pkg.PartitionedData(parts), pkg.LogisticGradient(), pkg.SimpleSGDUpdater(),
+                                  1.0, 1, 0.0, 1.0, np.array([0.1, 0.2]), 0.0)
+    wr, hr, _ = oracle.run(oracle.Matrix(y, X), [0, 0, 0, 2], "logistic", "simple", 1.0, 1, 0.0,
+                           np.array([0.1, 0.2]), tol=0.0)
+    assert np.all(np.isnan(w)) and np.all(np.isnan(wr))
+    assert_close(h, hr, what="loss")
+
+
+def test_device_registration_matches_host(pkg, oracle):
+    import torch
+    rng = np.random.default_rng(3)
+    n, d, P = 3000, 512, 6
+    X, y = synth(rng, n, d, "logistic", np.float32)
+    host = pkg.PartitionedData.parallelize(y, X, P, dtype=np.float32)
+    Xd = torch.from_numpy(X).cuda()
+    yd = torch.from_numpy(y).cuda()
+    offs = [i * n // P for i in range(P)] + [n]
+    dev = pkg.PartitionedData([pkg.DevicePartition(yd[a:b], Xd[a:b], d) for a, b in zip(offs[:-1], offs[1:])])
+    args = (pkg.LogisticGradient(), pkg.SimpleSGDUpdater(), 1.0, 2, 0.0, 1.0, np.zeros(d), 0.0)
+    w1, h1 = pkg.runParallelizedSGD(host, *args)
+    w2, h2 = pkg.runParallelizedSGD(dev, *args)
+    assert np.array_equal(w1, w2) and np.array_equal(h1, h2)
+
+
+def test_host_pointer_epoch_abi(pkg, oracle):
+    """psgd_run_epoch (the JNI-shaped call with host buffers) = one oracle iteration."""
+    rng = np.random.default_rng(4)
+    n, d, P = 900, 64, 3
+    X, y = synth(rng, n, d, "hinge")
+    ctx = pkg._native.Context(0)
+    offs = [i * n // P for i in range(P)] + [n]
+    for p in range(P):
+        ctx.register_dense(p, y[offs[p]:offs[p + 1]], X[offs[p]:offs[p + 1]])
+    prm = pkg.make_params(pkg.HingeGradient(), pkg.SimpleSGDUpdater(), 0.7, 0.0, 1.0, 0.0)
+    w, rv, loss, cnt, counts = ctx.run_epoch(prm, np.zeros(d))
+    wr, rvr, lr, cr = oracle.run_chains(oracle.Matrix(y, X), offs, "hinge", "simple", 0.7, 0.0, np.zeros(d))
+    assert list(counts) == list(cr) and cnt == n
+    acc_w, acc_c = wr[0].copy(), cr[0]
+    for p in range(1, P):
+        acc_w = (acc_w * acc_c + wr[p] * cr[p]) / (acc_c + cr[p])
+        acc_c += cr[p]
+    assert_close(w, acc_w, what="weights")
+    assert_close(loss, lr.sum(), what="loss")
+    ctx.close()
+
+
+def test_determinism_many_chains(pkg):
+    rng = np.random.default_rng(6)
+    n, d, P = 256 * 300, 512, 256
+    X, y = synth(rng, n, d, "least_squares", np.float32)
+    data = pkg.PartitionedData.parallelize(y, X, P, dtype=np.float32)
+    args = (pkg.LeastSquaresGradient(), pkg.SimpleSGDUpdater(), 1e-3, 2, 0.0, 1.0, np.zeros(d), 0.0)
+    w1, h1 = pkg.runParallelizedSGD(data, *args)
+    w2, h2 = pkg.runParallelizedSGD(data, *args)
+    assert np.array_equal(w1, w2) and np.array_equal(h1, h2)

@@ -1,0 +1,139 @@
+"""The CPU oracle: pinned against the reference suite's known-answer properties
+(ParallelizedSGDSuite.scala), cross-checked against the independent pure-Python restatement,
+and against the committed golden fixtures."""
+import math
+import random
+
+import numpy as np
+import pytest
+
+import psgd_ref as R
+
+
+def suite_data(O, n, bias_first=False):
+    x, y = O.generate_gd_input(2.0, -1.5, n, 42)
+    X = np.stack([np.ones(n), x], 1) if bias_first else np.stack([x, np.ones(n)], 1)
+    return X, y
+
+
+def test_generator_matches_python_restatement(oracle):
+    x, y = oracle.generate_gd_input(2.0, -1.5, 3000, 42)
+    xp, yp = R.generate_gd_input(2.0, -1.5, 3000, 42)
+    assert list(x) == xp and list(y) == yp
+
+
+def test_fdlibm_log_within_one_ulp_of_libm(oracle):
+    rs = random.Random(5)
+    for _ in range(20000):
+        v = rs.random() * 10 ** rs.uniform(-300, 300)
+        a, b = oracle.fdlibm_log(v), math.log(v)
+        assert a == R.fdlibm_log(v)
+        assert abs(a - b) <= math.ulp(b)
+    assert oracle.fdlibm_log(1.0) == 0.0 and oracle.fdlibm_log(0.0) == -math.inf
+
+
+def test_java_random_known_sequence(oracle):
+    # java.util.Random(42): nextDouble() published first value 0.7275636800328681
+    assert oracle.jrandom_doubles(42, 1)[0] == 0.7275636800328681
+    g = oracle.jrandom_gaussians(42, 2)
+    assert list(g) == [R.JavaRandom(42).next_gaussian(), g[1]]
+
+
+def test_suite_loss_decreasing(oracle):
+    """ParallelizedSGDSuite.scala:67-105 -- loss.last - loss.head < 0."""
+    X, y = suite_data(oracle, 10000)
+    w, h, c = oracle.run(oracle.Matrix(y, X), [0, 5000, 10000], "logistic", "simple", 1.0, 10,
+                         0.0, [-1.0, 1.0], tol=0.001)
+    assert len(h) == 10 and h[-1] - h[0] < 0
+    assert list(c[0]) == [153, 35]  # per-sample convergence breaks fire early
+
+
+def test_suite_first_iteration_with_regularization(oracle):
+    """ParallelizedSGDSuite.scala:107-142 -- L2: loss1 = loss0 + |w0|^2/2, w1 = w0' - w0."""
+    X, y = suite_data(oracle, 2, bias_first=True)
+    m = oracle.Matrix(y, X)
+    w0 = np.array([1.0, 0.5])
+    nw0, l0, _ = oracle.run(m, [0, 1, 2], "logistic", "squared_l2", 1.0, 1, 0.0, w0)
+    nw1, l1, _ = oracle.run(m, [0, 1, 2], "logistic", "squared_l2", 1.0, 1, 1.0, w0)
+    assert abs(l1[0] - (l0[0] + (w0[0] ** 2 + w0[1] ** 2) / 2)) < 1e-5
+    assert abs(nw1[0] - (nw0[0] - w0[0])) < 1e-5 and abs(nw1[1] - (nw0[1] - w0[1])) < 1e-5
+
+
+def test_suite_convergence_tolerance(oracle):
+    """ParallelizedSGDSuite.scala:144-181 -- tol 0.5 stops before numIterations."""
+    X, y = suite_data(oracle, 10000)
+    _, h, _ = oracle.run(oracle.Matrix(y, X), [0, 5000, 10000], "logistic", "simple", 1.0, 10,
+                         0.0, [-1.0, 1.0], tol=0.5)
+    assert len(h) < 10
+
+
+def test_survey_scratch_anchors_with_glibc_log(oracle, monkeypatch):
+    """SURVEY §8c anchors came from a scratch port that used libm log instead of StrictMath.log;
+    substituting it reproduces them bit for bit (so the chain/combine/driver logic agrees with
+    that independent port; the 1-ulp differences are the generator's log only)."""
+    monkeypatch.setattr(R, "fdlibm_log", math.log)
+    x, y = R.generate_gd_input(2.0, -1.5, 10000, 42)
+    assert x[:3] == [1.141905315473055, 0.919407948982788, -0.9498666368908959]
+    assert sum(y) / len(y) == 0.8133
+    parts = [([[1.0, x[0]]], [y[0]]), ([[1.0, x[1]]], [y[1]])]
+    w, h, _ = R.run(parts, 0, 1, 1.0, 1, 0.0, [1.0, 0.5])
+    assert w == [1.180296615483073, 0.6849098844205752] and h == [0.19886296441133905]
+    w, h, _ = R.run(parts, 0, 1, 1.0, 1, 1.0, [1.0, 0.5])
+    assert w == [0.18029661548307302, 0.18490988442057515] and h == [0.8238629644113391]
+
+
+@pytest.mark.parametrize("gi", range(3))
+@pytest.mark.parametrize("ui", range(5))
+def test_c_matches_python_bitwise_small(oracle, gi, ui):
+    rng = np.random.default_rng(100 + 10 * gi + ui)
+    n, d = 60, 5
+    X = rng.standard_normal((n, d))
+    y = (rng.uniform(size=n) > 0.5).astype(float) if gi != 1 else 0.3 * rng.standard_normal(n)
+    offs = [0, 20, 20, 60]
+    for tol in (0.0, 0.05):
+        w, h, c = oracle.run(oracle.Matrix(y, X), offs, gi, ui, 0.3, 3, 0.05, np.zeros(d), tol=tol)
+        parts = [([list(X[r]) for r in range(a, b)], list(y[a:b])) for a, b in zip(offs[:-1], offs[1:])]
+        wp, hp, cp = R.run(parts, gi, ui, 0.3, 3, 0.05, [0.0] * d, tol=tol)
+        assert list(w) == wp and list(h) == hp
+        assert [list(r) for r in c[:len(cp)]] == cp
+
+
+def test_two_level_combine_order(oracle):
+    rng = np.random.default_rng(3)
+    X = rng.standard_normal((90, 4))
+    y = (rng.uniform(size=90) > 0.5).astype(float)
+    offs = [0, 20, 45, 70, 90]
+    w, h, _ = oracle.run(oracle.Matrix(y, X), offs, "logistic", "simple", 0.5, 2, 0.0, np.zeros(4),
+                         tol=0.0, groups=[0, 2, 4])
+    parts = [([list(X[r]) for r in range(a, b)], list(y[a:b])) for a, b in zip(offs[:-1], offs[1:])]
+    wp, hp, _ = R.run(parts, 0, 0, 0.5, 2, 0.0, [0.0] * 4, tol=0.0, groups=[0, 2, 4])
+    assert list(w) == wp and list(h) == hp
+
+
+def test_empty_partitions_combine(oracle):
+    """Two empty partitions merged first give 0/0 = NaN weights (the reference's combiner,
+    ParallelizedSGD.scala:272-274); one empty partition merges harmlessly."""
+    X = np.array([[1.0, 2.0], [0.5, -1.0]])
+    y = np.array([1.0, 0.0])
+    m = oracle.Matrix(y, X)
+    w, h, _ = oracle.run(m, [0, 0, 2], "logistic", "simple", 1.0, 1, 0.0, [0.1, 0.2], tol=0.0)
+    assert np.all(np.isfinite(w)) and len(h) == 1
+    w, h, _ = oracle.run(m, [0, 0, 0, 2], "logistic", "simple", 1.0, 1, 0.0, [0.1, 0.2], tol=0.0)
+    assert np.all(np.isnan(w))
+
+
+def test_golden_fixtures_reproduce(oracle, golden):
+    for case in golden:
+        if case["source"] == "suite":
+            X, y = suite_data(oracle, case["n"], case["bias_first"])
+            m = oracle.Matrix(y, X)
+        elif "X" in case:
+            m = oracle.Matrix(np.array(case["y"]), np.array(case["X"]))
+        else:
+            m = oracle.Matrix(np.array(case["y"]), row_ptr=np.array(case["row_ptr"]),
+                              col=np.array(case["col"]), val=np.array(case["val"]), d=case["d"])
+        w, h, c = oracle.run(m, case["offsets"], case["gradient"], case["updater"], case["step"],
+                             case["iters"], case["reg"], np.array(case["w0"]), tol=case["tol"])
+        e = case["expected"]
+        assert list(map(float, w)) == e["weights"], case["name"]
+        assert list(map(float, h)) == e["loss_history"], case["name"]
