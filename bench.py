@@ -125,6 +125,7 @@ def main():
     if args.rows:
         n = args.rows
     X, y, offs = make_shard(torch, dev, n, d, P, grad, sdt, 1000 + rank)
+    torch.cuda.synchronize()
     parts = [pkg.DevicePartition(y[a:b], X[a:b], d) for a, b in zip(offs[:-1], offs[1:])]
     # global partition list: this rank's block is [rank*P, (rank+1)*P)
     all_parts = [None] * (P * world)
@@ -138,7 +139,7 @@ def main():
     params = pkg.make_params(gcls, pkg.SimpleSGDUpdater(), step, 0.0, 1.0, 0.0, args.compute)
     import numpy as np
     w = engine.weights(np.zeros(d))
-    stream = torch.cuda.current_stream(dev)
+    stream = engine.stream  # the engine's kernels and copies all run on this stream
 
     def one_step(w, it, ev=None):
         params.iteration = it
@@ -148,7 +149,7 @@ def main():
         if ev is not None:
             ev[1].record(stream)
         rv, loss, cnt = engine.scalars(folded)  # D2H of the 3 driver scalars (PSGD:278-287)
-        return engine.adopt(folded) if cnt > 0 else w, cnt, loss
+        return (engine.adopt(folded) if cnt > 0 else w), cnt, loss
 
     for i in range(args.warmup):
         w, cnt, loss = one_step(w, i + 1)
@@ -175,6 +176,8 @@ def main():
     # `cnt` is the whole job's sample count of the step (the fold sums counts over all ranks)
     samples_per_step = cnt
     value = samples_per_step * args.steps / elapsed
+    assert samples_per_step == n * world, (samples_per_step, n * world)
+    assert np.isfinite(loss), loss
     epoch_ms = [a.elapsed_time(b) for a, b in events]
     avg_epoch_s = sum(epoch_ms) / len(epoch_ms) / 1e3
     es = 4 if sdt == "f32" else 8

@@ -336,7 +336,11 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, in
         T x[E];
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
-            const V xv = *reinterpret_cast<const V*>(src + v * 1024 + lane * 16);
+            V xv = *reinterpret_cast<const V*>(src + v * 1024 + lane * 16);
+            if constexpr (!FULL) {
+                // vectors past the row end were not loaded: their LDS bytes are stale
+                if ((v * 64 + lane) * VEC >= dsc.ld) xv = V(0);
+            }
             unpack<S, T>(xv, x + v * VEC);
         }
         const f64x2 meta = *reinterpret_cast<const f64x2*>(src + ROW_BYTES);

@@ -106,6 +106,9 @@ class HipEngine:
         self.device = device
         self.dev = torch.device("cuda", device)
         self.ctx = get_context(device)
+        # Every kernel of this engine and every torch op on its buffers runs on this stream
+        # (a real stream handle: NULL would select the library's own stream).
+        self.stream = torch.cuda.Stream(device=self.dev)
         self.d = data.num_features
         self.rank, self.world = rank, world
         self.lo, self.hi = shard_range(data.num_partitions, rank, world)
@@ -142,7 +145,8 @@ class HipEngine:
 
     # driver hooks ---------------------------------------------------------------------------
     def weights(self, w_host: np.ndarray):
-        return self.torch.from_numpy(np.ascontiguousarray(w_host, dtype=np.float64)).to(self.dev)
+        with self.torch.cuda.stream(self.stream):
+            return self.torch.from_numpy(np.ascontiguousarray(w_host, dtype=np.float64)).to(self.dev)
 
     def initial_regval(self, params, w_host: np.ndarray) -> float:
         return self.ctx.initial_regval(params, w_host)
@@ -150,7 +154,13 @@ class HipEngine:
     def epoch(self, params, w_dev, with_counts: bool = False):
         """PSGD.scala:238-276 for all ranks: returns the folded (d+3) device vector
         [w_avg, regVal, lossSum, count] and (optionally) this rank's chain counts."""
-        stream = self.torch.cuda.current_stream(self.dev).cuda_stream
+        # order after whatever produced the inputs on the caller's stream
+        self.stream.wait_stream(self.torch.cuda.current_stream(self.dev))
+        with self.torch.cuda.stream(self.stream):
+            return self._epoch(params, w_dev, with_counts)
+
+    def _epoch(self, params, w_dev, with_counts):
+        stream = self.stream.cuda_stream
         if self.n_local > 0:
             self.ctx.run_epoch_device(params, w_dev.data_ptr(), self._partial.data_ptr(),
                                       self._counts.data_ptr() if with_counts else None, stream)
@@ -170,18 +180,21 @@ class HipEngine:
         return out, counts
 
     def scalars(self, folded) -> Tuple[float, float, int]:
-        h = folded[self.d:].cpu().numpy()
+        with self.torch.cuda.stream(self.stream):
+            h = folded[self.d:].cpu().numpy()
         return float(h[0]), float(h[1]), int(h[2])
 
     def adopt(self, folded):
-        return folded[: self.d].clone()
+        with self.torch.cuda.stream(self.stream):
+            return folded[: self.d].clone()
 
     def convergence_terms(self, prev, cur) -> Tuple[float, float]:
-        stream = self.torch.cuda.current_stream(self.dev).cuda_stream
-        return self.ctx.convergence_terms_device(self.d, prev.data_ptr(), cur.data_ptr(), stream)
+        return self.ctx.convergence_terms_device(self.d, prev.data_ptr(), cur.data_ptr(),
+                                                 self.stream.cuda_stream)
 
     def to_host(self, w_dev) -> np.ndarray:
-        return w_dev.detach().cpu().numpy().astype(np.float64)
+        with self.torch.cuda.stream(self.stream):
+            return w_dev.detach().cpu().numpy().astype(np.float64)
 
 
 # ---------------------------------------------------------------------------------------------
