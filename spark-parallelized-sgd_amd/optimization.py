@@ -120,6 +120,12 @@ class HipEngine:
             token = uuid.uuid4().hex
             data._psgd_token = token
         key = (token, self.lo, self.hi)
+        self.n_local = self.hi - self.lo
+        self._partial = self.torch.empty(self.d + 3, dtype=self.torch.float64, device=self.dev)
+        self._gather = (self.torch.empty(self.world * (self.d + 3), dtype=self.torch.float64,
+                                         device=self.dev) if self.world > 1 else None)
+        self._folded = self.torch.empty(self.d + 3, dtype=self.torch.float64, device=self.dev)
+        self._counts = self.torch.empty(max(self.n_local, 1), dtype=self.torch.int64, device=self.dev)
         if self.ctx.registered_token == key:
             return
         self.ctx.clear()
@@ -136,12 +142,6 @@ class HipEngine:
             else:
                 raise IllegalArgumentException(f"unsupported partition type {type(part).__name__}")
         self.ctx.registered_token = key
-        self._partial = self.torch.empty(self.d + 3, dtype=self.torch.float64, device=self.dev)
-        self._gather = (self.torch.empty(self.world * (self.d + 3), dtype=self.torch.float64,
-                                         device=self.dev) if self.world > 1 else None)
-        self._folded = self.torch.empty(self.d + 3, dtype=self.torch.float64, device=self.dev)
-        self.n_local = self.hi - self.lo
-        self._counts = self.torch.empty(max(self.n_local, 1), dtype=self.torch.int64, device=self.dev)
 
     # driver hooks ---------------------------------------------------------------------------
     def weights(self, w_host: np.ndarray):
