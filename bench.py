@@ -85,24 +85,28 @@ def cpu_baseline(grad, d, P, step, budget_s, seed=7):
             ((z + rng.logistic(size=P * m)) > 0).astype(float)
         return X, y
 
-    # calibrate on a tiny sample, then size the timed sample to ~budget_s
-    m = 16
+    # A sample of m rows per partition (host memory bounded), re-run as successive epochs until
+    # the time budget is spent: per-epoch CPU cost does not depend on which rows are used.
+    m = 1024 if d <= 1024 else 256
     X, y = sample(m)
     offs = [p * m for p in range(P + 1)]
+    mat = O.Matrix(y, X)
+    w = np.zeros(d)
+    total, epochs = 0, 0
     t0 = time.perf_counter()
-    O.run_chains(O.Matrix(y, X), offs, grad, "simple", step, 0.0, np.zeros(d), tol=0.0, n_threads=cores)
-    dt = max(time.perf_counter() - t0, 1e-3)
-    m = int(max(16, min(4096, m * budget_s / dt)))
-    X, y = sample(m)
-    offs = [p * m for p in range(P + 1)]
-    t0 = time.perf_counter()
-    _, _, _, cnt = O.run_chains(O.Matrix(y, X), offs, grad, "simple", step, 0.0, np.zeros(d),
-                                tol=0.0, n_threads=cores)
-    dt = time.perf_counter() - t0
-    return {"value": float(cnt.sum()) / dt, "unit": "samples/s", "cores": cores, "kind": "port",
+    while True:
+        w_out, _, _, cnt = O.run_chains(mat, offs, grad, "simple", step, 0.0, w, tol=0.0,
+                                        n_threads=cores)
+        total += int(cnt.sum())
+        epochs += 1
+        w = w_out.mean(axis=0)
+        dt = time.perf_counter() - t0
+        if dt >= budget_s:
+            break
+    return {"value": total / dt, "unit": "samples/s", "cores": cores, "kind": "port",
             "sample": f"oracle/psgd_oracle.c (fp64 CPU restatement of ParallelizedSGD.scala:243-270 "
-                      f"incl. per-sample isConverged), {P} partitions x first {m} rows, d={d}, "
-                      f"{cores} threads, {dt:.1f} s"}
+                      f"incl. per-sample isConverged), {P} partitions x {m} rows, d={d}, "
+                      f"{epochs} epochs, {cores} threads, {dt:.1f} s"}
 
 
 def main():

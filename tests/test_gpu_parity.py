@@ -176,7 +176,9 @@ def test_fp32_compute_mode_tolerance(pkg, oracle, grad, d):
     X, y = synth(rng, n, d, grad, np.float32)
     data = pkg.PartitionedData.parallelize(y, X, P, dtype=np.float32)
     offs = [i * n // P for i in range(P)] + [n]
-    step = 1e-3 if grad == "least_squares" else 1.0
+    # a well-conditioned step (||x||^2 ~ d): at step 1.0 a d=1024 logistic chain is chaotic and
+    # fp32 vs fp64 trajectories separate for reasons unrelated to the kernel
+    step = 1e-3 if grad == "least_squares" else 0.01
     w, h = pkg.runParallelizedSGD(data, getattr(pkg, G[grad])(), pkg.SimpleSGDUpdater(), step, 3, 0.0,
                                   1.0, np.zeros(d), 0.0, compute_dtype="f32")
     wr, hr, _ = oracle.run(oracle.Matrix(y, X.astype(np.float64)), offs, grad, "simple", step, 3, 0.0,
