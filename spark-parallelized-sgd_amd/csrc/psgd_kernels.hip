@@ -308,7 +308,11 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, in
     }
 
     // ---------------- compute ----------------
-    T w[E];
+    // Weights and rows are held as pairs (T2) so that fp32 runs on packed VALU ops
+    // (v_pk_fma/mul/add_f32: two IEEE-rounded lanes per instruction).
+    using T2 = T __attribute__((ext_vector_type(2)));
+    constexpr int E2 = E / 2;
+    T2 w[E2];
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
         const int base = (v * 64 + lane) * VEC;
@@ -316,24 +320,16 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, in
         for (int k = 0; k < VEC; ++k) {
             const int f = base + k;
             const double wv = as_global(L.w_in)[f < d ? f : 0];  // unconditional, clamped
-            w[v * VEC + k] = f < d ? T(wv) : T(0);
+            w[(v * VEC + k) / 2][(v * VEC + k) % 2] = f < d ? T(wv) : T(0);
         }
     }
 
-    double loss_sum = 0.0;
-    int64_t count = 0;
-    unsigned ready = 0;
-    int slot = 0;
-    for (int64_t t = 0; t < n; ++t) {
-        if (t >= (int64_t)ready) {
-            for (;;) {
-                ready = __hip_atomic_load(&hdr->ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (t < (int64_t)ready) break;
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
-        const char* src = ring + slot * SLOT_BYTES;
-        T x[E];
+    // Row buffers: two register copies (ping-pong) so row t+1's LDS reads are in flight while
+    // sample t computes.
+    T2 xb[2][E2];
+    double yb[2], sb[2];
+    auto read_row = [&](auto pc, const char* src) __attribute__((always_inline)) {
+        constexpr int p = decltype(pc)::value;
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
             V xv = *reinterpret_cast<const V*>(src + v * 1024 + lane * 16);
@@ -341,70 +337,116 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, in
                 // vectors past the row end were not loaded: their LDS bytes are stale
                 if ((v * 64 + lane) * VEC >= dsc.ld) xv = V(0);
             }
-            unpack<S, T>(xv, x + v * VEC);
+            T tmp[VEC];
+            unpack<S, T>(xv, tmp);
+#pragma unroll
+            for (int k = 0; k < VEC; k += 2) xb[p][(v * VEC + k) / 2] = T2{tmp[k], tmp[k + 1]};
         }
         const f64x2 meta = *reinterpret_cast<const f64x2*>(src + ROW_BYTES);
-        const T y = T(meta.x);
-        const T s = T(meta.y);
-        if (++slot == R) slot = 0;
+        yb[p] = meta.x;
+        sb[p] = meta.y;
+    };
+
+    unsigned ready = 0;
+    auto wait_rows = [&](int64_t rows) __attribute__((always_inline)) {
+        if (rows > (int64_t)ready) {
+            for (;;) {
+                ready = __hip_atomic_load(&hdr->ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (rows <= (int64_t)ready) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+    };
+
+    double loss_sum = 0.0;
+    T loss_blk = T(0);          // fp32 mode: block partial, flushed to the fp64 sum every 32 rows
+    int64_t count = 0;
+    bool stop = false;
+    const char* slot_ptr = ring;                       // slot of row t
+    const char* const ring_end = ring + R * SLOT_BYTES;
+
+    auto sample = [&](auto pc, int64_t t) __attribute__((always_inline)) {
+        constexpr int p = decltype(pc)::value;
+        const char* next_ptr = slot_ptr + SLOT_BYTES;
+        if (next_ptr == ring_end) next_ptr = ring;
+        if (t + 1 < n) {   // prefetch row t+1 into the other buffer
+            wait_rows(t + 2);
+            read_row(std::integral_constant<int, 1 - p>{}, next_ptr);
+        }
+        const T y = T(yb[p]);
+        const T s = T(sb[p]);
+        const T2* x = xb[p];
 
         // dot(data, weights)
-        T acc0 = T(0), acc1 = T(0);
+        T2 acc0 = T2{T(0), T(0)}, acc1 = T2{T(0), T(0)};
 #pragma unroll
-        for (int e = 0; e < E; e += 2) {
-            acc0 = m_fma(x[e], w[e], acc0);
-            if (e + 1 < E) acc1 = m_fma(x[e + 1], w[e + 1], acc1);
+        for (int e = 0; e < E2; e += 2) {
+            acc0 = __builtin_elementwise_fma(x[e], w[e], acc0);
+            if (e + 1 < E2) acc1 = __builtin_elementwise_fma(x[e + 1], w[e + 1], acc1);
         }
-        // the slot has been read (x feeds the FMAs above): hand it back to the loader
-        __hip_atomic_store(&hdr->consumed, (unsigned)(t + 1), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_WORKGROUP);
-        const T z = wave_sum(acc0 + acc1);
+        const T2 acc = acc0 + acc1;
+        const T z = wave_sum(acc.x + acc.y);
+        if ((t & 3) == 3 || t + 1 == n) {
+            // rows <= t have been read into registers: hand their slots back to the loader
+            __hip_atomic_store(&hdr->consumed, (unsigned)(t + 1), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
 
         T mult;
         const T loss = gradient_scalar<GRAD, T>(z, y, mult);
-        loss_sum += double(loss);
+        if constexpr (sizeof(T) == 4) {
+            loss_blk += loss;
+            if ((t & 31) == 31) { loss_sum += double(loss_blk); loss_blk = T(0); }
+        } else {
+            loss_sum += loss;
+        }
         count += 1;
 
         const T a = -s;
-        T dsq = T(0), nsq = T(0);
-        if constexpr (UPD == U_SQUARED_L2) {
-            const T c = T(1) - s * T(kp.reg);
+        T2 dsq2 = T2{T(0), T(0)}, nsq2 = T2{T(0), T(0)};
 #pragma unroll
-            for (int e = 0; e < E; ++e) {
-                const T old = w[e];
-                T nw = old * c;
-                nw = nw + a * (mult * x[e]);
-                w[e] = nw;
-                if constexpr (CONV) { const T df = old - nw; dsq += df * df; nsq += nw * nw; }
+        for (int e = 0; e < E2; ++e) {
+            const T2 old = w[e];
+            T2 nw;
+            if constexpr (UPD == U_SQUARED_L2) {
+                const T c = T(1) - s * T(kp.reg);
+                nw = old * c;                       // brzWeights :*= (1 - s*lambda)
+                nw = nw + a * (mult * x[e]);        // axpy(-s, grad, w)
+            } else if constexpr (UPD == U_L1) {
+                const T shrink = T(kp.reg) * s;
+                nw = old + a * (mult * x[e]);
+                nw.x = jsignum(nw.x) * jmax(T(0), m_fabs(nw.x) - shrink);
+                nw.y = jsignum(nw.y) * jmax(T(0), m_fabs(nw.y) - shrink);
+            } else {
+                nw = old + a * (mult * x[e]);
             }
-        } else if constexpr (UPD == U_L1) {
-            const T shrink = T(kp.reg) * s;
-#pragma unroll
-            for (int e = 0; e < E; ++e) {
-                const T old = w[e];
-                T nw = old + a * (mult * x[e]);
-                nw = jsignum(nw) * jmax(T(0), m_fabs(nw) - shrink);
-                w[e] = nw;
-                if constexpr (CONV) { const T df = old - nw; dsq += df * df; nsq += nw * nw; }
-            }
-        } else {
-#pragma unroll
-            for (int e = 0; e < E; ++e) {
-                const T old = w[e];
-                const T nw = old + a * (mult * x[e]);
-                w[e] = nw;
-                if constexpr (CONV) { const T df = old - nw; dsq += df * df; nsq += nw * nw; }
-            }
+            w[e] = nw;
+            if constexpr (CONV) { const T2 df = old - nw; dsq2 += df * df; nsq2 += nw * nw; }
         }
+        slot_ptr = next_ptr;
         if constexpr (CONV) {
+            T dsq = dsq2.x + dsq2.y, nsq = nsq2.x + nsq2.y;
             wave_sum2(dsq, nsq);
             // ||old - new|| < tol * max(||new||, 1.0)   (PSGD.scala:262, :333-335)
             if (m_sqrt(dsq) < T(kp.tol) * jmax(m_sqrt(nsq), T(1))) {
                 __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                break;
+                stop = true;
             }
         }
+    };
+
+    if (n > 0) {
+        wait_rows(1);
+        read_row(std::integral_constant<int, 0>{}, ring);
     }
+    int64_t t = 0;
+    for (; t + 2 <= n && !stop; t += 2) {
+        sample(std::integral_constant<int, 0>{}, t);
+        if constexpr (CONV) { if (stop) break; }
+        sample(std::integral_constant<int, 1>{}, t + 1);
+    }
+    if (t < n && !stop) sample(std::integral_constant<int, 0>{}, t);
+    if constexpr (sizeof(T) == 4) loss_sum += double(loss_blk);
 
     // regVal of the chain's last update (PSGD.scala:257; 0.0 if no sample, :247)
     double rv = 0.0;
@@ -412,8 +454,9 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, in
         T acc = T(0);
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-            if constexpr (UPD == U_SQUARED_L2) acc += w[e] * w[e];
-            else acc += m_fabs(w[e]);
+            const T we = w[e / 2][e % 2];
+            if constexpr (UPD == U_SQUARED_L2) acc += we * we;
+            else acc += m_fabs(we);
         }
         acc = wave_sum(acc);
         if (count > 0) {
@@ -432,7 +475,7 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, in
         const int base = (v * 64 + lane) * VEC;
 #pragma unroll
         for (int k = 0; k < VEC; ++k)
-            if (base + k < d) wo[base + k] = double(w[v * VEC + k]);
+            if (base + k < d) wo[base + k] = double(w[(v * VEC + k) / 2][(v * VEC + k) % 2]);
     }
     if (lane == 0) {
         L.rv[chain] = rv;
