@@ -12,12 +12,13 @@ from ._native import (DeviceError, IllegalArgumentException, UnsupportedOperatio
                       build)
 from .data import CsrPartition, DensePartition, DevicePartition, PartitionedData, shard_range
 from .gradient import Gradient, HingeGradient, LeastSquaresGradient, LogisticGradient
-from .optimization import HipEngine, ParallelizedSGD, make_params, runParallelizedSGD
+from .optimization import (HipEngine, ParallelizedSGD, ShardedEngine, make_params,
+                           runParallelizedSGD)
 from .updater import (AdaGradSGDUpdater, AdamSGDUpdater, L1SGDUpdater, SGDUpdater,
                       SimpleSGDUpdater, SquaredL2SGDUpdater)
 
 __all__ = [
-    "ParallelizedSGD", "runParallelizedSGD", "HipEngine", "make_params",
+    "ParallelizedSGD", "runParallelizedSGD", "HipEngine", "ShardedEngine", "make_params",
     "Gradient", "LogisticGradient", "LeastSquaresGradient", "HingeGradient",
     "SGDUpdater", "SimpleSGDUpdater", "SquaredL2SGDUpdater", "L1SGDUpdater",
     "AdaGradSGDUpdater", "AdamSGDUpdater",

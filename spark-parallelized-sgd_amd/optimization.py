@@ -75,7 +75,7 @@ def _dist():
 
 
 # ---------------------------------------------------------------------------------------------
-# HIP engine: device-resident weights, one psgd_ctx per process.
+# Engines: who runs the chains of this process's partitions.
 # ---------------------------------------------------------------------------------------------
 _contexts = {}
 
@@ -89,29 +89,68 @@ def get_context(device: int) -> N.Context:
     return ctx
 
 
-class HipEngine:
-    """Runs the chains of this process's partitions on one MI355X (psgd C ABI).
+class ShardedEngine:
+    """The multi-process part of an epoch, shared by every engine.
 
-    Weights and the (d+3)-double partial results stay in HBM (torch tensors used only as
-    device allocations and as the RCCL all-gather buffers)."""
+    Partition p belongs to rank floor(p * world / P) (contiguous blocks). Each rank
+    folds its own chains (partition order) into a (d+3)-vector [w, regVal, lossSum, count];
+    the ranks all-gather those partials and fold them in rank order with the reference's
+    combiner -- a two-level treeReduce (ParallelizedSGD.scala:271-276). A rank without
+    partitions contributes the fold's identity element (w_in, 0, 0, 0): an empty partition's
+    result (ParallelizedSGD.scala:270 with count 0)."""
+
+    def __init__(self, data: PartitionedData, rank: int, world: int):
+        self.d = data.num_features
+        self.rank, self.world = rank, world
+        self.lo, self.hi = shard_range(data.num_partitions, rank, world)
+        self.n_local = self.hi - self.lo
+
+    # subclass hooks: local_partial(params, w, with_counts) -> (partial[d+3], counts | None);
+    # empty_partial(w) -> partial; fold_partials(gathered[world*(d+3)]) -> partial;
+    # gather_buffer() -> tensor[world*(d+3)]
+    def epoch(self, params, w, with_counts: bool = False):
+        """ParallelizedSGD.scala:238-276 over all ranks: the folded [w_avg, regVal, lossSum,
+        count] and (optionally) this rank's chain counts."""
+        if self.n_local > 0:
+            partial, counts = self.local_partial(params, w, with_counts)
+        else:
+            partial, counts = self.empty_partial(w), None
+        if self.world == 1:
+            return partial, counts
+        import torch.distributed as dist
+        out = self.gather_buffer()
+        if dist.get_backend() == "gloo":
+            dist.all_gather(list(out.view(self.world, self.d + 3).unbind(0)), partial)
+        else:
+            dist.all_gather_into_tensor(out, partial)
+        return self.fold_partials(out), counts
+
+
+class HipEngine(ShardedEngine):
+    """Runs this process's chains on one MI355X through the psgd C ABI.
+
+    Weights and the (d+3)-double partial results stay in HBM (torch tensors serve as device
+    allocations and as the RCCL all-gather buffers); every kernel and copy runs on
+    `self.stream`."""
 
     def __init__(self, data: PartitionedData, rank: int = 0, world: int = 1,
                  device: Optional[int] = None):
         import torch
         if not torch.cuda.is_available():
             raise N.DeviceError("HipEngine needs a visible MI355X (torch.cuda.is_available() is False)")
+        super().__init__(data, rank, world)
         if device is None:
             device = torch.cuda.current_device()
         self.torch = torch
         self.device = device
         self.dev = torch.device("cuda", device)
         self.ctx = get_context(device)
-        # Every kernel of this engine and every torch op on its buffers runs on this stream
-        # (a real stream handle: NULL would select the library's own stream).
+        # a real stream handle: NULL would select the library's own stream
         self.stream = torch.cuda.Stream(device=self.dev)
-        self.d = data.num_features
-        self.rank, self.world = rank, world
-        self.lo, self.hi = shard_range(data.num_partitions, rank, world)
+        self._partial = torch.empty(self.d + 3, dtype=torch.float64, device=self.dev)
+        self._gather = torch.empty(self.world * (self.d + 3), dtype=torch.float64, device=self.dev)
+        self._folded = torch.empty(self.d + 3, dtype=torch.float64, device=self.dev)
+        self._counts = torch.empty(max(self.n_local, 1), dtype=torch.int64, device=self.dev)
         self._register(data)
 
     def _register(self, data: PartitionedData):
@@ -120,15 +159,10 @@ class HipEngine:
             token = uuid.uuid4().hex
             data._psgd_token = token
         key = (token, self.lo, self.hi)
-        self.n_local = self.hi - self.lo
-        self._partial = self.torch.empty(self.d + 3, dtype=self.torch.float64, device=self.dev)
-        self._gather = (self.torch.empty(self.world * (self.d + 3), dtype=self.torch.float64,
-                                         device=self.dev) if self.world > 1 else None)
-        self._folded = self.torch.empty(self.d + 3, dtype=self.torch.float64, device=self.dev)
-        self._counts = self.torch.empty(max(self.n_local, 1), dtype=self.torch.int64, device=self.dev)
         if self.ctx.registered_token == key:
             return
         self.ctx.clear()
+        self.ctx.registered_token = None
         for p in range(self.lo, self.hi):
             part = data.partitions[p]
             if isinstance(part, DensePartition):
@@ -152,32 +186,30 @@ class HipEngine:
         return self.ctx.initial_regval(params, w_host)
 
     def epoch(self, params, w_dev, with_counts: bool = False):
-        """PSGD.scala:238-276 for all ranks: returns the folded (d+3) device vector
-        [w_avg, regVal, lossSum, count] and (optionally) this rank's chain counts."""
         # order after whatever produced the inputs on the caller's stream
         self.stream.wait_stream(self.torch.cuda.current_stream(self.dev))
         with self.torch.cuda.stream(self.stream):
-            return self._epoch(params, w_dev, with_counts)
+            return super().epoch(params, w_dev, with_counts)
 
-    def _epoch(self, params, w_dev, with_counts):
-        stream = self.stream.cuda_stream
-        if self.n_local > 0:
-            self.ctx.run_epoch_device(params, w_dev.data_ptr(), self._partial.data_ptr(),
-                                      self._counts.data_ptr() if with_counts else None, stream)
-        if self.world == 1:
-            out = self._partial
-        else:
-            import torch.distributed as dist
-            if self.n_local == 0:
-                # an empty rank contributes the identity of the fold: (w_in, 0, 0, 0)
-                self._partial[: self.d].copy_(w_dev)
-                self._partial[self.d:].zero_()
-            dist.all_gather_into_tensor(self._gather, self._partial)
-            self.ctx.fold_partials_device(self.world, self.d, self._gather.data_ptr(),
-                                          self._folded.data_ptr(), stream)
-            out = self._folded
+    def local_partial(self, params, w_dev, with_counts):
+        self.ctx.run_epoch_device(params, w_dev.data_ptr(), self._partial.data_ptr(),
+                                  self._counts.data_ptr() if with_counts else None,
+                                  self.stream.cuda_stream)
         counts = self._counts[: self.n_local].cpu().numpy() if with_counts else None
-        return out, counts
+        return self._partial, counts
+
+    def empty_partial(self, w_dev):
+        self._partial[: self.d].copy_(w_dev)
+        self._partial[self.d:].zero_()
+        return self._partial
+
+    def gather_buffer(self):
+        return self._gather
+
+    def fold_partials(self, gathered):
+        self.ctx.fold_partials_device(self.world, self.d, gathered.data_ptr(),
+                                      self._folded.data_ptr(), self.stream.cuda_stream)
+        return self._folded
 
     def scalars(self, folded) -> Tuple[float, float, int]:
         with self.torch.cuda.stream(self.stream):
