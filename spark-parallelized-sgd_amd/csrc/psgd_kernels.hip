@@ -87,6 +87,40 @@ __device__ __forceinline__ T wave_sum(T v) {
     return v;
 }
 
+// Wave sum delivered as a wave-uniform value: four DPP row steps, then row_bcast:15 / :31 fold
+// the four row sums into lane 63 ((r3 + r2) + (r1 + r0)), which v_readlane broadcasts. Two
+// fewer instructions than the swap form and the result lands in SGPRs for the scalar math.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_mov_rows(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWS, 0xF, false));
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_mov_rows(double v) {
+    long long b = __double_as_longlong(v);
+    int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, ROWS, 0xF, false);
+    int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWS, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ float readlane63(float v) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ __forceinline__ double readlane63(double v) {
+    long long b = __double_as_longlong(v);
+    int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), 63);
+    int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <typename T>
+__device__ __forceinline__ T wave_sum_uniform(T v) {
+    v = v + dpp_mov<0xB1>(v);            // quad_perm [1,0,3,2]
+    v = v + dpp_mov<0x4E>(v);            // quad_perm [2,3,0,1]
+    v = v + dpp_mov<0x141>(v);           // row_half_mirror
+    v = v + dpp_mov<0x140>(v);           // row_mirror: every lane holds its row's sum
+    v = v + dpp_mov_rows<0x142, 0xA>(v); // row_bcast:15 -> rows 1, 3 hold r0+r1, r2+r3
+    v = v + dpp_mov_rows<0x143, 0xC>(v); // row_bcast:31 -> row 3 holds the total
+    return readlane63(v);
+}
+
 // Two independent sums reduced together (ILP for the convergence terms).
 template <typename T>
 __device__ __forceinline__ void wave_sum2(T& a, T& b) {
@@ -385,15 +419,22 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, in
             if (e + 1 < E2) acc1 = __builtin_elementwise_fma(x[e + 1], w[e + 1], acc1);
         }
         const T2 acc = acc0 + acc1;
-        const T z = wave_sum(acc.x + acc.y);
+        const T z = wave_sum_uniform(acc.x + acc.y);
         if ((t & 3) == 3 || t + 1 == n) {
             // rows <= t have been read into registers: hand their slots back to the loader
             __hip_atomic_store(&hdr->consumed, (unsigned)(t + 1), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
         }
 
-        T mult;
-        const T loss = gradient_scalar<GRAD, T>(z, y, mult);
+        T mult, loss;
+        if constexpr (GRAD == G_LEAST_SQUARES) {
+            // loss = diff*diff/2.0: the halving is exact, so the chain accumulates diff*diff and
+            // halves the sum (identical to summing the halves)
+            mult = z - y;
+            loss = mult * mult;
+        } else {
+            loss = gradient_scalar<GRAD, T>(z, y, mult);
+        }
         if constexpr (sizeof(T) == 4) {
             loss_blk += loss;
             if ((t & 31) == 31) { loss_sum += double(loss_blk); loss_blk = T(0); }
@@ -417,8 +458,11 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, in
                 nw = old + a * (mult * x[e]);
                 nw.x = jsignum(nw.x) * jmax(T(0), m_fabs(nw.x) - shrink);
                 nw.y = jsignum(nw.y) * jmax(T(0), m_fabs(nw.y) - shrink);
+            } else if constexpr (sizeof(T) == 4) {
+                // fp32 throughput mode: one fused update per pair, w + (-s*mult) * x
+                nw = __builtin_elementwise_fma(T2{a * mult, a * mult}, x[e], old);
             } else {
-                nw = old + a * (mult * x[e]);
+                nw = old + a * (mult * x[e]);   // the reference's two roundings (fp64 mode)
             }
             w[e] = nw;
             if constexpr (CONV) { const T2 df = old - nw; dsq2 += df * df; nsq2 += nw * nw; }
@@ -447,6 +491,7 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, in
     }
     if (t < n && !stop) sample(std::integral_constant<int, 0>{}, t);
     if constexpr (sizeof(T) == 4) loss_sum += double(loss_blk);
+    if constexpr (GRAD == G_LEAST_SQUARES) loss_sum = loss_sum / 2.0;
 
     // regVal of the chain's last update (PSGD.scala:257; 0.0 if no sample, :247)
     double rv = 0.0;
