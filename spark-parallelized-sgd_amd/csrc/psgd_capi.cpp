@@ -87,7 +87,7 @@ struct psgd_ctx {
     std::mutex mu;
     std::map<int64_t, Part> parts;
     bool descs_dirty = true;
-    DevBuf descs, w_in, w_out, state, rv, loss, cnt_d, cnt, steps, partial, tmp;
+    DevBuf descs, w_in, w_out, state, rv, loss, cnt_d, cnt, steps, partial, tmp, watchdog;
     double steps_value = NAN;
     int64_t steps_n = 0;
     int32_t last_variant = 0;
@@ -166,6 +166,7 @@ int32_t prepare(psgd_ctx* ctx, int32_t d, bool need_state, hipStream_t st) {
     HIP_TRY(ctx->cnt.ensure(std::max<size_t>(P, 1) * sizeof(int64_t)));
     HIP_TRY(ctx->partial.ensure(((size_t)std::max(d, 1) + 3) * sizeof(double)));
     HIP_TRY(ctx->tmp.ensure(((size_t)std::max(d, 1) + 8) * sizeof(double)));
+    HIP_TRY(ctx->watchdog.ensure(16));
     if (need_state)
         HIP_TRY(ctx->state.ensure(std::max<size_t>(P, 1) * 2 * (size_t)std::max(d, 1) *
                                   sizeof(double)));
@@ -260,7 +261,8 @@ int32_t psgd_ctx_destroy(psgd_ctx* ctx) {
         hipStreamSynchronize(ctx->stream);
         for (auto& kv : ctx->parts) free_part(kv.second);
         for (DevBuf* b : {&ctx->descs, &ctx->w_in, &ctx->w_out, &ctx->state, &ctx->rv, &ctx->loss,
-                          &ctx->cnt_d, &ctx->cnt, &ctx->steps, &ctx->partial, &ctx->tmp})
+                          &ctx->cnt_d, &ctx->cnt, &ctx->steps, &ctx->partial, &ctx->tmp,
+                          &ctx->watchdog})
             b->release();
         hipStreamDestroy(ctx->stream);
     }
@@ -464,6 +466,8 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
     L.cnt_d = ctx->cnt_d.as<double>();
     L.cnt = ctx->cnt.as<int64_t>();
     L.steps = ctx->steps.as<double>();
+    L.watchdog = ctx->watchdog.as<int>();
+    HIP_TRY(hipMemsetAsync(L.watchdog, 0, 16, st));
     psgd::KParams kp;
     kp.reg = params->reg_param;
     kp.tol = params->convergence_tol;
@@ -491,7 +495,7 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         if (e) return fail(PSGD_EDEVICE, std::string("chain kernel launch failed: ") +
                                              hipGetErrorString((hipError_t)e));
     }
-    int e = psgd::launch_fold(L.w_out, d, L.rv, L.loss, L.cnt_d, 1, P, d, d_partial, st);
+    int e = psgd::launch_fold(L.w_out, d, L.rv, L.loss, L.cnt_d, 1, P, d, d_partial, L.watchdog, st);
     if (e) return fail(PSGD_EDEVICE, "fold kernel launch failed");
     if (d_chain_counts)
         HIP_TRY(hipMemcpyAsync(d_chain_counts, L.cnt, (size_t)P * sizeof(int64_t),
@@ -540,6 +544,8 @@ int32_t psgd_run_epoch(psgd_ctx* ctx, const psgd_params* params, const double* w
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     counts.release();
     std::memcpy(w_out, h.data(), (size_t)d * sizeof(double));
+    if (h[(size_t)d + 2] != h[(size_t)d + 2])
+        return fail(PSGD_EDEVICE, "chain kernel watchdog fired (loader/compute waves stalled)");
     if (regval_out) *regval_out = h[(size_t)d];
     if (loss_sum_out) *loss_sum_out = h[(size_t)d + 1];
     if (count_out) *count_out = (int64_t)h[(size_t)d + 2];
@@ -554,7 +560,7 @@ int32_t psgd_fold_partials_device(psgd_ctx* ctx, int32_t n, int32_t d, const dou
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     const int64_t stride = (int64_t)d + 3;
     int e = psgd::launch_fold(d_partials, stride, d_partials + d, d_partials + d + 1,
-                              d_partials + d + 2, stride, n, d, d_out, st);
+                              d_partials + d + 2, stride, n, d, d_out, nullptr, st);
     if (e) return fail(PSGD_EDEVICE, "fold kernel launch failed");
     return PSGD_OK;
 }

@@ -39,6 +39,7 @@ struct ChainLaunch {
     double* cnt_d;           // [n_chains]  count as double (exact < 2^53) for the fold
     int64_t* cnt;            // [n_chains]  count
     const double* steps;     // [n_max] stepSize / sqrt(j), j = 1..n_max
+    int* watchdog;           // set by a wave whose partner stopped making progress
 };
 
 // Host-side launchers implemented in psgd_kernels.hip. Return hipError_t as int.
@@ -48,7 +49,7 @@ int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int stora
                   int lds_spread, hipStream_t stream, int* kernel_variant);
 int launch_fold(const double* w, int64_t w_stride, const double* rv, const double* loss,
                 const double* cnt, int64_t s_stride, int n, int d, double* out,
-                hipStream_t stream);
+                const int* watchdog, hipStream_t stream);
 int launch_sq_terms(const double* a, const double* b, int d, double* out2, hipStream_t stream);
 int launch_steps(double step, int64_t n, double* steps, hipStream_t stream);
 

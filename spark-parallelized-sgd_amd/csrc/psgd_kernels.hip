@@ -249,7 +249,10 @@ struct RingHeader {
     unsigned stop;      // compute wave left the chain early (per-sample convergence break)
     unsigned pad;
 };
-constexpr int kMetaBytes = 256;  // one dword per lane of the meta DMA; bytes 0..15 = {y, step}
+constexpr int kMetaBytes = 256;
+// s_memrealtime runs at 100 MHz: a wave that sees no progress from its partner for 4 s sets the
+// launch's watchdog word and leaves (the host then raises instead of hanging).
+constexpr uint64_t kWatchdogTicks = 400000000ull;  // one dword per lane of the meta DMA; bytes 0..15 = {y, step}
 
 __device__ __forceinline__ unsigned lds_load_u32_asm(const unsigned* p) {
     unsigned v;
@@ -303,14 +306,27 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, in
         // meta: lanes 0/1 -> label lo/hi, 2/3 -> step lo/hi (other lanes duplicate)
         const unsigned* ysrc = reinterpret_cast<const unsigned*>((lane & 2) ? L.steps : dsc.y) + (lane & 1);
         unsigned consumed = 0;
+        int64_t published = 0;
         int slot = 0;
         for (int64_t t = 0; t < n; ++t) {
             if (t >= (int64_t)consumed + R) {
-                // wait for the compute wave to free the slot of row t - R
+                // Ring full. Everything issued so far lands before we block: publish it, so the
+                // compute wave can never wait on rows that sit behind this wait.
+                asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
+                if (t > published) {
+                    published = t;
+                    lds_store_u32_asm(&hdr->ready, (unsigned)t);
+                }
+                // wait for the compute wave to free the slot of row t - R (bounded spin)
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
                 for (;;) {
                     consumed = lds_load_u32_asm(&hdr->consumed);
                     if (t < (int64_t)consumed + R) break;
                     if (lds_load_u32_asm(&hdr->stop)) goto drain;
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > kWatchdogTicks) {
+                        __hip_atomic_fetch_or(L.watchdog, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        goto drain;
+                    }
                     __builtin_amdgcn_s_sleep(2);
                 }
             }
@@ -329,10 +345,11 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, in
                                                  4, 0, 0);
             }
             if (++slot == R) slot = 0;
-            if (t >= D) {
+            if (t >= D && t - D + 1 > published) {
                 // the oldest of the D rows in flight (row t - D) has landed
                 asm volatile("s_waitcnt vmcnt(%0)" : : "n"(D * (NV + 1)) : "memory");
-                lds_store_u32_asm(&hdr->ready, (unsigned)(t - D + 1));
+                published = t - D + 1;
+                lds_store_u32_asm(&hdr->ready, (unsigned)published);
             }
         }
     drain:
@@ -382,20 +399,29 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, in
     };
 
     unsigned ready = 0;
-    auto wait_rows = [&](int64_t rows) __attribute__((always_inline)) {
+    bool stop = false;
+    // Wait until `rows` rows have landed; false (and the watchdog flag) if the loader makes no
+    // progress for kWatchdogTicks.
+    auto wait_rows = [&](int64_t rows) __attribute__((always_inline)) -> bool {
         if (rows > (int64_t)ready) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             for (;;) {
                 ready = __hip_atomic_load(&hdr->ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (rows <= (int64_t)ready) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kWatchdogTicks) {
+                    __hip_atomic_fetch_or(L.watchdog, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    return false;
+                }
                 __builtin_amdgcn_s_sleep(1);
             }
         }
+        return true;
     };
 
     double loss_sum = 0.0;
     T loss_blk = T(0);          // fp32 mode: block partial, flushed to the fp64 sum every 32 rows
     int64_t count = 0;
-    bool stop = false;
     const char* slot_ptr = ring;                       // slot of row t
     const char* const ring_end = ring + R * SLOT_BYTES;
 
@@ -404,7 +430,7 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, in
         const char* next_ptr = slot_ptr + SLOT_BYTES;
         if (next_ptr == ring_end) next_ptr = ring;
         if (t + 1 < n) {   // prefetch row t+1 into the other buffer
-            wait_rows(t + 2);
+            if (!wait_rows(t + 2)) { stop = true; return; }
             read_row(std::integral_constant<int, 1 - p>{}, next_ptr);
         }
         const T y = T(yb[p]);
@@ -420,7 +446,7 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, in
         }
         const T2 acc = acc0 + acc1;
         const T z = wave_sum_uniform(acc.x + acc.y);
-        if ((t & 3) == 3 || t + 1 == n) {
+        if ((t & 1) == 1 || t + 1 == n) {
             // rows <= t have been read into registers: hand their slots back to the loader
             __hip_atomic_store(&hdr->consumed, (unsigned)(t + 1), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -480,13 +506,13 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, in
     };
 
     if (n > 0) {
-        wait_rows(1);
-        read_row(std::integral_constant<int, 0>{}, ring);
+        if (wait_rows(1)) read_row(std::integral_constant<int, 0>{}, ring);
+        else stop = true;
     }
     int64_t t = 0;
     for (; t + 2 <= n && !stop; t += 2) {
         sample(std::integral_constant<int, 0>{}, t);
-        if constexpr (CONV) { if (stop) break; }
+        if (stop) break;
         sample(std::integral_constant<int, 1>{}, t + 1);
     }
     if (t < n && !stop) sample(std::integral_constant<int, 0>{}, t);
@@ -742,7 +768,7 @@ __global__ __launch_bounds__(64) void chain_general(ChainLaunch L, KParams kp) {
 __global__ void fold_kernel(const double* __restrict__ w, int64_t w_stride,
                             const double* __restrict__ rv, const double* __restrict__ loss,
                             const double* __restrict__ cnt, int64_t s_stride, int n, int d,
-                            double* __restrict__ out) {
+                            double* __restrict__ out, const int* __restrict__ watchdog) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < d) {
         double acc = w[i];
@@ -763,7 +789,8 @@ __global__ void fold_kernel(const double* __restrict__ w, int64_t w_stride,
         }
         out[d] = r;
         out[d + 1] = l;
-        out[d + 2] = c1;
+        // a chain kernel that tripped its watchdog poisons the count: the host raises
+        out[d + 2] = (watchdog && *watchdog) ? __builtin_nan("") : c1;
     }
 }
 
@@ -806,9 +833,13 @@ static int launch_reg(const ChainLaunch& L, const KParams& kp, bool full, size_t
     // LDS ring: header + R slots of (row + meta). `lds` is the per-workgroup budget chosen by
     // the host (it also spreads the chains over the CUs).
     constexpr int SLOT = NV * 1024 + kMetaBytes;
+    // at least 12 slots (rows t, t+1 held by the compute wave, a consumed lag of 1, the rest in
+    // flight), at most what a CU's 160 KiB allows
     size_t budget = lds > 0 ? lds : (size_t)64 * 1024;
     int rows = (int)((budget - sizeof(RingHeader)) / SLOT);
-    if (rows < 2) rows = 2;
+    if (rows < 12) rows = 12;
+    if (sizeof(RingHeader) + (size_t)rows * SLOT > (size_t)160 * 1024)
+        rows = (int)((160 * 1024 - sizeof(RingHeader)) / SLOT);
     const size_t bytes = sizeof(RingHeader) + (size_t)rows * SLOT;
     if (full) {
         auto k = chain_dense<S, T, GRAD, UPD, CONV, NV, true>;
@@ -909,12 +940,12 @@ int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int stora
 
 int launch_fold(const double* w, int64_t w_stride, const double* rv, const double* loss,
                 const double* cnt, int64_t s_stride, int n, int d, double* out,
-                hipStream_t stream) {
+                const int* watchdog, hipStream_t stream) {
     if (n <= 0) return -1;
     const int threads = 256;
     const int blocks = (d + 1 + threads - 1) / threads;
     hipLaunchKernelGGL(fold_kernel, dim3(blocks), dim3(threads), 0, stream, w, w_stride, rv, loss,
-                       cnt, s_stride, n, d, out);
+                       cnt, s_stride, n, d, out, watchdog);
     return (int)hipGetLastError();
 }
 

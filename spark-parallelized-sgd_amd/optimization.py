@@ -214,6 +214,8 @@ class HipEngine(ShardedEngine):
     def scalars(self, folded) -> Tuple[float, float, int]:
         with self.torch.cuda.stream(self.stream):
             h = folded[self.d:].cpu().numpy()
+        if not math.isfinite(h[2]):
+            raise N.DeviceError("chain kernel watchdog fired (loader/compute waves stalled)")
         return float(h[0]), float(h[1]), int(h[2])
 
     def adopt(self, folded):
