@@ -205,18 +205,17 @@ int32_t ensure_steps(psgd_ctx* ctx, double step, int64_t n, hipStream_t st) {
     return PSGD_OK;
 }
 
-// Dynamic LDS request used only to spread chains evenly over the CUs (a CU admits
-// floor(160 KiB / request) chain workgroups). PSGD_LDS_SPREAD=0 disables it.
+// Per-workgroup LDS budget for the dense chain kernel's row ring: as deep a ring as possible
+// while floor(160 KiB / budget) chain workgroups fit per CU, so P chains spread evenly over
+// the CUs (one per CU for P <= #CUs). PSGD_LDS_BUDGET overrides (bytes).
 int lds_spread_bytes(const psgd_ctx* ctx, size_t P) {
-    const char* env = getenv("PSGD_LDS_SPREAD");
+    const char* env = getenv("PSGD_LDS_BUDGET");
     if (env) return std::max(0, atoi(env));
     if (P == 0) return 0;
     const size_t per_cu = (P + (size_t)ctx->num_cus - 1) / (size_t)ctx->num_cus;
-    if (per_cu > 8) return 0;
     const size_t lds_total = 160 * 1024;
-    size_t want = lds_total / (per_cu + 1) + 1024;  // per_cu fit, per_cu + 1 do not
-    want = std::min<size_t>(want, 64 * 1024);
-    return (int)(want & ~(size_t)1023);
+    size_t want = lds_total / std::max<size_t>(per_cu, 1) - 512;
+    return (int)(want & ~(size_t)255);
 }
 
 }  // namespace

@@ -249,10 +249,34 @@ struct RingHeader {
     unsigned stop;      // compute wave left the chain early (per-sample convergence break)
     unsigned pad;
 };
-constexpr int kMetaBytes = 256;
+// Labels and steps travel in 256-byte meta blocks, one per 16 rows: {y, stepSize/sqrt(j)} x 16.
+constexpr int kMetaRows = 16;
+constexpr int kMetaBlockBytes = 256;
 // s_memrealtime runs at 100 MHz: a wave that sees no progress from its partner for 4 s sets the
 // launch's watchdog word and leaves (the host then raises instead of hanging).
-constexpr uint64_t kWatchdogTicks = 400000000ull;  // one dword per lane of the meta DMA; bytes 0..15 = {y, step}
+constexpr uint64_t kWatchdogTicks = 400000000ull;
+
+// s_waitcnt vmcnt(k) for a runtime k (the immediate must be a constant).
+__device__ __forceinline__ void wait_vmcnt_le(int k) {
+#define PSGD_VMCNT_CASE(K) case K: asm volatile("s_waitcnt vmcnt(" #K ")" ::: "memory"); break;
+    switch (k) {
+        PSGD_VMCNT_CASE(0) PSGD_VMCNT_CASE(1) PSGD_VMCNT_CASE(2) PSGD_VMCNT_CASE(3)
+        PSGD_VMCNT_CASE(4) PSGD_VMCNT_CASE(5) PSGD_VMCNT_CASE(6) PSGD_VMCNT_CASE(7)
+        PSGD_VMCNT_CASE(8) PSGD_VMCNT_CASE(10) PSGD_VMCNT_CASE(12) PSGD_VMCNT_CASE(14)
+        PSGD_VMCNT_CASE(16) PSGD_VMCNT_CASE(20) PSGD_VMCNT_CASE(24) PSGD_VMCNT_CASE(28)
+        PSGD_VMCNT_CASE(32) PSGD_VMCNT_CASE(36) PSGD_VMCNT_CASE(40) PSGD_VMCNT_CASE(44)
+        PSGD_VMCNT_CASE(48) PSGD_VMCNT_CASE(52) PSGD_VMCNT_CASE(56) PSGD_VMCNT_CASE(60)
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+#undef PSGD_VMCNT_CASE
+}
+
+// Ring geometry chosen by the launcher (psgd_kernels.hip, launch_reg).
+struct RingGeom {
+    int rows;         // R row slots
+    int meta_blocks;  // MB meta blocks (16 rows each)
+    int depth;        // D: rows the loader keeps in flight past the oldest unpublished one
+};
 
 __device__ __forceinline__ unsigned lds_load_u32_asm(const unsigned* p) {
     unsigned v;
@@ -265,23 +289,17 @@ __device__ __forceinline__ void lds_store_u32_asm(unsigned* p, unsigned v) {
     asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : : "v"(addr), "v"(v) : "memory");
 }
 
-template <int NV>
-__device__ __forceinline__ constexpr int loader_depth() {
-    // rows in flight before the loader waits for the oldest: (NV + 1) VMEM instructions per
-    // row, vmcnt counts at most 63.
-    return 60 / (NV + 1);
-}
-
 template <typename S, typename T, int GRAD, int UPD, bool CONV, int NV, bool FULL>
-__global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, int ring_rows) {
+__global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, RingGeom geom) {
     using V = typename Vec16<S>::type;
     constexpr int VEC = Vec16<S>::N;
     constexpr int E = NV * VEC;
     constexpr int ROW_BYTES = NV * 1024;
-    constexpr int SLOT_BYTES = ROW_BYTES + kMetaBytes;
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    // LDS: [header 16 B][meta ring MB x 256 B][row ring R x ROW_BYTES]
     RingHeader* hdr = reinterpret_cast<RingHeader*>(smem);
-    char* ring = smem + sizeof(RingHeader);
+    char* meta_ring = smem + sizeof(RingHeader);
+    char* ring = meta_ring + geom.meta_blocks * kMetaBlockBytes;
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -289,7 +307,8 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, in
     const ChainDesc dsc = L.descs[chain];
     const int d = kp.d;
     const int64_t n = dsc.n_rows;
-    const int R = ring_rows;
+    const int R = geom.rows;
+    const int MB = geom.meta_blocks;
 
     if (threadIdx.x == 0) {
         hdr->ready = 0;
@@ -300,24 +319,19 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, in
 
     if (wave == 1) {
         // ---------------- loader ----------------
-        constexpr int D = loader_depth<NV>();
+        const int D = geom.depth;
         const S* X = reinterpret_cast<const S*>(dsc.x);
         const int64_t ld = dsc.ld;
-        // meta: lanes 0/1 -> label lo/hi, 2/3 -> step lo/hi (other lanes duplicate)
-        const unsigned* ysrc = reinterpret_cast<const unsigned*>((lane & 2) ? L.steps : dsc.y) + (lane & 1);
+        // meta DMA lane l: row 16k + l/4, dword l%4 of {y lo, y hi, step lo, step hi}
+        const unsigned* msrc = reinterpret_cast<const unsigned*>((lane & 2) ? L.steps : dsc.y) + (lane & 1);
+        const int mrow = lane >> 2;
         unsigned consumed = 0;
         int64_t published = 0;
-        int slot = 0;
+        int slot = 0, mslot = 0;
         for (int64_t t = 0; t < n; ++t) {
             if (t >= (int64_t)consumed + R) {
-                // Ring full. Everything issued so far lands before we block: publish it, so the
-                // compute wave can never wait on rows that sit behind this wait.
-                asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
-                if (t > published) {
-                    published = t;
-                    lds_store_u32_asm(&hdr->ready, (unsigned)t);
-                }
-                // wait for the compute wave to free the slot of row t - R (bounded spin)
+                // ring full: wait for the compute wave to free the slot of row t - R
+                // (R - D >= 8 keeps enough rows published that this cannot deadlock)
                 const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
                 for (;;) {
                     consumed = lds_load_u32_asm(&hdr->consumed);
@@ -327,11 +341,19 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, in
                         __hip_atomic_fetch_or(L.watchdog, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         goto drain;
                     }
-                    __builtin_amdgcn_s_sleep(2);
+                    __builtin_amdgcn_s_sleep(1);
                 }
             }
+            if ((t & (kMetaRows - 1)) == 0) {
+                int64_t r = t + mrow;
+                if (r >= n) r = n - 1;
+                __builtin_amdgcn_global_load_lds(
+                    (const void*)(as_global(msrc + 2 * r)),
+                    (__attribute__((address_space(3))) void*)(meta_ring + mslot * kMetaBlockBytes), 4, 0, 0);
+                if (++mslot == MB) mslot = 0;
+            }
             {
-                char* dst = ring + slot * SLOT_BYTES;
+                char* dst = ring + slot * ROW_BYTES;
                 const V* row = reinterpret_cast<const V*>(X + t * ld);
 #pragma unroll
                 for (int v = 0; v < NV; ++v) {
@@ -340,14 +362,11 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, in
                             (const void*)(as_global(row + v * 64 + lane)),
                             (__attribute__((address_space(3))) void*)(dst + v * 1024), 16, 0, 0);
                 }
-                __builtin_amdgcn_global_load_lds((const void*)(as_global(ysrc + 2 * t)),
-                                                 (__attribute__((address_space(3))) void*)(dst + ROW_BYTES),
-                                                 4, 0, 0);
             }
             if (++slot == R) slot = 0;
-            if (t >= D && t - D + 1 > published) {
-                // the oldest of the D rows in flight (row t - D) has landed
-                asm volatile("s_waitcnt vmcnt(%0)" : : "n"(D * (NV + 1)) : "memory");
+            if (t >= D) {
+                // all but the newest D rows' instructions are done: row t - D has landed
+                wait_vmcnt_le(D * NV);
                 published = t - D + 1;
                 lds_store_u32_asm(&hdr->ready, (unsigned)published);
             }
@@ -379,7 +398,7 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, in
     // sample t computes.
     T2 xb[2][E2];
     double yb[2], sb[2];
-    auto read_row = [&](auto pc, const char* src) __attribute__((always_inline)) {
+    auto read_row = [&](auto pc, const char* src, int64_t t) __attribute__((always_inline)) {
         constexpr int p = decltype(pc)::value;
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
@@ -393,7 +412,8 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, in
 #pragma unroll
             for (int k = 0; k < VEC; k += 2) xb[p][(v * VEC + k) / 2] = T2{tmp[k], tmp[k + 1]};
         }
-        const f64x2 meta = *reinterpret_cast<const f64x2*>(src + ROW_BYTES);
+        const f64x2 meta = *reinterpret_cast<const f64x2*>(
+            meta_ring + ((t / kMetaRows) % MB) * kMetaBlockBytes + (t % kMetaRows) * 16);
         yb[p] = meta.x;
         sb[p] = meta.y;
     };
@@ -423,15 +443,15 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, in
     T loss_blk = T(0);          // fp32 mode: block partial, flushed to the fp64 sum every 32 rows
     int64_t count = 0;
     const char* slot_ptr = ring;                       // slot of row t
-    const char* const ring_end = ring + R * SLOT_BYTES;
+    const char* const ring_end = ring + R * ROW_BYTES;
 
     auto sample = [&](auto pc, int64_t t) __attribute__((always_inline)) {
         constexpr int p = decltype(pc)::value;
-        const char* next_ptr = slot_ptr + SLOT_BYTES;
+        const char* next_ptr = slot_ptr + ROW_BYTES;
         if (next_ptr == ring_end) next_ptr = ring;
         if (t + 1 < n) {   // prefetch row t+1 into the other buffer
             if (!wait_rows(t + 2)) { stop = true; return; }
-            read_row(std::integral_constant<int, 1 - p>{}, next_ptr);
+            read_row(std::integral_constant<int, 1 - p>{}, next_ptr, t + 1);
         }
         const T y = T(yb[p]);
         const T s = T(sb[p]);
@@ -506,7 +526,7 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, in
     };
 
     if (n > 0) {
-        if (wait_rows(1)) read_row(std::integral_constant<int, 0>{}, ring);
+        if (wait_rows(1)) read_row(std::integral_constant<int, 0>{}, ring, 0);
         else stop = true;
     }
     int64_t t = 0;
@@ -830,25 +850,37 @@ __global__ void steps_kernel(double step, int64_t n, double* __restrict__ steps)
 // ------------------------------------------------------------------------------------------
 template <typename S, typename T, int GRAD, int UPD, bool CONV, int NV>
 static int launch_reg(const ChainLaunch& L, const KParams& kp, bool full, size_t lds, hipStream_t st) {
-    // LDS ring: header + R slots of (row + meta). `lds` is the per-workgroup budget chosen by
-    // the host (it also spreads the chains over the CUs).
-    constexpr int SLOT = NV * 1024 + kMetaBytes;
-    // at least 12 slots (rows t, t+1 held by the compute wave, a consumed lag of 1, the rest in
-    // flight), at most what a CU's 160 KiB allows
-    size_t budget = lds > 0 ? lds : (size_t)64 * 1024;
-    int rows = (int)((budget - sizeof(RingHeader)) / SLOT);
-    if (rows < 12) rows = 12;
-    if (sizeof(RingHeader) + (size_t)rows * SLOT > (size_t)160 * 1024)
-        rows = (int)((160 * 1024 - sizeof(RingHeader)) / SLOT);
-    const size_t bytes = sizeof(RingHeader) + (size_t)rows * SLOT;
+    // Ring geometry from the per-workgroup LDS budget (`lds`: chosen by the host so that the
+    // chains spread evenly over the CUs). D rows stay in flight beyond the newest published row
+    // (vmcnt holds at most 63 instructions, NV per row); R - D >= 8 slots stay published or
+    // free so neither wave can wait on the other forever.
+    constexpr int ROW = NV * 1024;
+    const size_t budget = lds > 0 ? lds : (size_t)64 * 1024;
+    int D = 56 / NV;
+    if (D > 32) D = 32;
+    int R = 0, MB = 0;
+    for (;;) {
+        // rows that fit: header + meta blocks + rows
+        R = (int)((budget - sizeof(RingHeader) - 3 * kMetaBlockBytes) / ROW);
+        MB = (R + kMetaRows - 1) / kMetaRows + 2;
+        while (R > 0 && sizeof(RingHeader) + (size_t)MB * kMetaBlockBytes + (size_t)R * ROW > budget) {
+            --R;
+            MB = (R + kMetaRows - 1) / kMetaRows + 2;
+        }
+        if (R >= D + 8 || D == 1) break;
+        D = D > 2 ? D / 2 : 1;
+    }
+    if (R < D + 3) return (int)hipErrorInvalidValue;  // LDS budget too small for this d
+    RingGeom g{R, MB, D};
+    const size_t bytes = sizeof(RingHeader) + (size_t)MB * kMetaBlockBytes + (size_t)R * ROW;
     if (full) {
         auto k = chain_dense<S, T, GRAD, UPD, CONV, NV, true>;
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-        hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(128), bytes, st, L, kp, rows);
+        hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(128), bytes, st, L, kp, g);
     } else {
         auto k = chain_dense<S, T, GRAD, UPD, CONV, NV, false>;
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-        hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(128), bytes, st, L, kp, rows);
+        hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(128), bytes, st, L, kp, g);
     }
     return (int)hipGetLastError();
 }
