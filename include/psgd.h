@@ -142,8 +142,13 @@ int32_t psgd_initial_regval(psgd_ctx* ctx, const psgd_params* params, int32_t d,
                             double* regval_out);
 
 /* Diagnostics: which chain kernel the last epoch launched (101/102/104/108 = register-resident
- * dense kernel with NV 16-byte vectors per lane; 200 = general dense; 201 = general CSR). */
+ * dense kernel with NV 16-byte vectors per lane; 200 = general dense; 201 = general CSR;
+ * 301/302/304/308 = blocked fp32 dense kernel with NV 16-byte vectors per lane). */
 int32_t psgd_ctx_last_kernel(psgd_ctx* ctx);
+
+/* Diagnostics: device time of the last chain-kernel launch in milliseconds, from HIP events
+ * recorded around it on the launch stream (waits for that launch to finish). */
+int32_t psgd_ctx_last_chain_ms(psgd_ctx* ctx, double* ms_out);
 
 #ifdef __cplusplus
 }

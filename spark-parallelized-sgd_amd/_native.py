@@ -23,7 +23,7 @@ EXPORTED = (
     "psgd_register_dense", "psgd_register_csr", "psgd_register_dense_device",
     "psgd_clear_partitions", "psgd_num_partitions", "psgd_run_epoch", "psgd_run_epoch_device",
     "psgd_fold_partials_device", "psgd_convergence_terms_device", "psgd_initial_regval",
-    "psgd_ctx_last_kernel",
+    "psgd_ctx_last_kernel", "psgd_ctx_last_chain_ms",
 )
 
 
@@ -91,6 +91,7 @@ def lib():
             "psgd_convergence_terms_device": ([vp, C.c_int32, vp, vp, dp, vp], C.c_int32),
             "psgd_initial_regval": ([vp, P, C.c_int32, vp, dp], C.c_int32),
             "psgd_ctx_last_kernel": ([vp], C.c_int32),
+            "psgd_ctx_last_chain_ms": ([vp, dp], C.c_int32),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -170,6 +171,12 @@ class Context:
 
     def last_kernel(self) -> int:
         return int(self._L.psgd_ctx_last_kernel(self.handle))
+
+    def last_chain_ms(self) -> float:
+        """Device time of the last chain-kernel launch (HIP events on its stream)."""
+        ms = C.c_double()
+        check(self._L.psgd_ctx_last_chain_ms(self.handle, C.byref(ms)))
+        return ms.value
 
     # epochs ---------------------------------------------------------------------------------
     def run_epoch_device(self, params, w_ptr, partial_ptr, counts_ptr=None, stream=None):

@@ -1,0 +1,559 @@
+// psgd_block.hip -- the blocked chain kernel of the fp32 throughput mode (gfx950).
+//
+// Reference: ParallelizedSGD.scala:243-270 (the chain), [ext] MLlib 1.6.1 Gradient.scala
+// (Logistic / LeastSquares / Hinge multipliers, called at ParallelizedSGD.scala:254),
+// SGDUpdater.scala:86-98 (SimpleSGDUpdater) and :163-181 (SquaredL2SGDUpdater).
+//
+// The chain is sequential: w_{t+1} = a_t w_t + c_t x_t with c_t = -s_t * mult(x_t . w_t, y_t),
+// s_t = stepSize/sqrt(t+1), a_t = 1 (Simple) or 1 - s_t*lambda (SquaredL2). Done sample by sample
+// the critical path of every sample is a 512-long dot, a cross-lane reduction and the update
+// (~100 dependent cycles), which caps one chain per CU well below the HBM rate. Over a block of
+// K = 8 consecutive rows with weights W at its start the same recurrence is exactly
+//
+//     p_k = x_k . W                       (K independent dots against one W)
+//     G[k][i] = x_k . x_i, i < k          (the block's Gram triangle, independent of W)
+//     z_0 = p_0;  acc_k <- a_i acc_k + c_i G[k][i]  after step i;  z_k = acc_k after step k-1
+//     W'  = a_{K-1}(...(a_0 W + c_0 x_0)...) + c_{K-1} x_{K-1}
+//
+// so the only sequential work left per sample is scalar (c_i from z_i, one FMA per lane). The
+// rounding differs from the per-sample form (dot products reassociated, updates fused), which
+// is the fp32 throughput mode's stated tolerance; the fp64 parity mode keeps the
+// per-sample kernels of psgd_kernels.hip.
+//
+// One workgroup = one chain = four waves, one per SIMD:
+//   wave 0 (chain)   owns W in VGPRs (lane l: features (v*64+l)*VEC ..), per block: reads the K
+//                    rows from the LDS ring, the K dots (packed FMAs + one transposed reduction
+//                    of 8 values), the scalar recurrence with the Gram row of its lane, the loss,
+//                    and the K updates;
+//   wave 1 (loader)  LDS-DMA row ring (ring_loader, shared with chain_dense);
+//   waves 2, 3 (Gram) alternate blocks: the 28 pair dots of a block (packed FMAs + a transposed
+//                    reduction of 32 values), written as an 8x8 lower-triangular matrix into a
+//                    Gram ring slot in LDS.
+// No MFMA: the Gram triangle is 3.5 dots per row; a 16x16 f32 MFMA tile would spend 16.
+#include "psgd_device.h"
+
+namespace psgd {
+
+constexpr int kBlk = 8;           // rows per block
+constexpr int kPairs = 28;        // kBlk*(kBlk-1)/2 Gram entries below the diagonal
+
+struct GramHeader {
+    unsigned gdone[2];   // blocks finished by Gram wave 0 (even blocks) / 1 (odd blocks)
+    unsigned pad[2];
+};
+
+// --- transposed wave reductions -----------------------------------------------------------
+// Several per-lane partial sums are reduced at once: every stage halves the number of values a
+// lane carries and doubles the lanes each value is summed over. permlane32_swap(x, y) leaves
+// {x.lo|y.lo} and {x.hi|y.hi}: their sum holds x's total over the two halves in lanes 0-31 and
+// y's in lanes 32-63. permlane16_swap does the same for odd/even rows of 16 lanes.
+__device__ __forceinline__ float pair32(float x, float y) {
+    auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+    return __uint_as_float(p[0]) + __uint_as_float(p[1]);
+}
+__device__ __forceinline__ float pair16(float x, float y) {
+    auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+    return __uint_as_float(p[0]) + __uint_as_float(p[1]);
+}
+// Inside a row: lanes with `bit` clear keep x, the others y; each adds its DPP partner's copy.
+template <int CTRL, int BIT>
+__device__ __forceinline__ float pair_dpp(float x, float y, int lane) {
+    const bool hi = (lane & BIT) != 0;
+    const float keep = hi ? y : x;
+    const float send = hi ? x : y;
+    return keep + dpp_mov<CTRL>(send);
+}
+
+// 8 values -> lane l holds the total of value k(l) = l5 | l4<<1 | l3<<2 (lane bits).
+__device__ __forceinline__ float reduce8(const float (&v)[8], int lane) {
+    const float a0 = pair32(v[0], v[1]), a1 = pair32(v[2], v[3]);
+    const float a2 = pair32(v[4], v[5]), a3 = pair32(v[6], v[7]);
+    const float b0 = pair16(a0, a1), b1 = pair16(a2, a3);
+    float r = pair_dpp<0x140, 8>(b0, b1, lane);   // row_mirror: partner l^15
+    r = r + dpp_mov<0xB1>(r);                      // quad_perm [1,0,3,2]: l^1
+    r = r + dpp_mov<0x4E>(r);                      // quad_perm [2,3,0,1]: l^2
+    r = r + dpp_mov<0x141>(r);                     // row_half_mirror: l^7
+    return r;
+}
+// 32 values -> lane l holds the total of value j(l) = l5 | l4<<1 | l3<<2 | l2<<3 | l1<<4.
+__device__ __forceinline__ float reduce32(const float (&v)[32], int lane) {
+    float a[16], b[8], c[4], e[2];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) a[m] = pair32(v[2 * m], v[2 * m + 1]);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) b[m] = pair16(a[2 * m], a[2 * m + 1]);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) c[m] = pair_dpp<0x140, 8>(b[2 * m], b[2 * m + 1], lane);   // l^15
+#pragma unroll
+    for (int m = 0; m < 2; ++m) e[m] = pair_dpp<0x141, 4>(c[2 * m], c[2 * m + 1], lane);   // l^7
+    float r = pair_dpp<0x4E, 2>(e[0], e[1], lane);                                           // l^2
+    return r + dpp_mov<0xB1>(r);                                                             // l^1
+}
+
+// Lane that carries row i of a block after reduce8 (any lane with k(l) = i; this one has l&7 = 0).
+__host__ __device__ constexpr int row_lane(int i) {
+    return 32 * (i & 1) + 16 * ((i >> 1) & 1) + 8 * ((i >> 2) & 1);
+}
+
+__device__ __forceinline__ float readlane_f(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+// c = -s * mult(z, y) for the gradient (vector form; only lane row_lane(i) matters at step i).
+//   Logistic: mult = 1/(1+exp(-z)) - y;  LeastSquares: mult = z - y;  Hinge: mult = 1 > ls*z ? -ls : 0
+template <int GRAD>
+__device__ __forceinline__ float coef(float z, float y, float s, float ns, float aux) {
+    if constexpr (GRAD == G_LEAST_SQUARES) {
+        return __builtin_fmaf(ns, z, aux);            // aux = s*y: -s*z + s*y
+    } else if constexpr (GRAD == G_LOGISTIC) {
+        const float e = __expf(-z);
+        const float sig = __builtin_amdgcn_rcpf(1.0f + e);
+        return ns * (sig - y);
+    } else {
+        return (aux * z < 1.0f) ? s * aux : 0.0f;     // aux = ls = 2y - 1: -s * (-ls)
+    }
+}
+
+template <int GRAD>
+__device__ __forceinline__ float row_loss(float z, float y, float aux) {
+    if constexpr (GRAD == G_LEAST_SQUARES) {
+        const float m = z - y;
+        return m * m;                                  // halved once at the end (exact)
+    } else if constexpr (GRAD == G_LOGISTIC) {
+        const float margin = -z;
+        const float l = log1p_exp(margin);
+        return y > 0.0f ? l : l - margin;
+    } else {
+        const float lz = aux * z;
+        return (1.0f > lz) ? 1.0f - lz : 0.0f;
+    }
+}
+
+template <typename S, int GRAD, int UPD, int NV, bool FULL>
+__global__ __launch_bounds__(256) void chain_block(ChainLaunch L, KParams kp, RingGeom geom) {
+    using V = typename Vec16<S>::type;
+    using T2 = float __attribute__((ext_vector_type(2)));
+    constexpr int VEC = Vec16<S>::N;
+    constexpr int E = NV * VEC;            // features per lane
+    constexpr int E2 = E / 2;
+    constexpr int H = VEC / 2;             // pairs per 16-byte vector
+    constexpr int ROW_BYTES = NV * 1024;
+    constexpr bool KEEP = E2 * kBlk <= 64; // the chain wave keeps a block's rows in registers
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    // LDS: [RingHeader 16 B][GramHeader 16 B][meta ring MB x 256 B][Gram ring GS x 256 B]
+    //      [row ring R x ROW_BYTES]
+    RingHeader* hdr = reinterpret_cast<RingHeader*>(smem);
+    GramHeader* ghdr = reinterpret_cast<GramHeader*>(smem + sizeof(RingHeader));
+    char* meta_ring = smem + sizeof(RingHeader) + sizeof(GramHeader);
+    float* gring = reinterpret_cast<float*>(meta_ring + geom.meta_blocks * kMetaBlockBytes);
+    const int GS = geom.gslots;
+    char* ring = reinterpret_cast<char*>(gring + GS * kBlk * kBlk);
+
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int chain = blockIdx.x;
+    const ChainDesc dsc = L.descs[chain];
+    const int d = kp.d;
+    const int64_t n = dsc.n_rows;
+    const int R = geom.rows;               // multiple of kBlk: a block never wraps
+    const int MB = geom.meta_blocks;
+    const int64_t nblk = (n + kBlk - 1) / kBlk;
+
+    if (threadIdx.x == 0) {
+        hdr->ready = 0;
+        hdr->consumed = 0;
+        hdr->stop = 0;
+        ghdr->gdone[0] = 0;
+        ghdr->gdone[1] = 0;
+    }
+    // entries on and above the diagonal stay zero (the Gram waves write only i < k)
+    for (int i = threadIdx.x; i < GS * kBlk * kBlk; i += blockDim.x) gring[i] = 0.0f;
+    __syncthreads();
+
+    if (wave == 1) {
+        ring_loader<S, NV, FULL>(L, dsc, hdr, meta_ring, ring, geom, lane);
+        return;
+    }
+
+    // Wait until `rows` rows have landed. false (and the watchdog) if nothing moves for 4 s.
+    auto wait_ready = [&](unsigned& ready, int64_t rows, int code) __attribute__((always_inline)) -> bool {
+        if (rows <= (int64_t)ready) return true;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            ready = __hip_atomic_load(&hdr->ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (rows <= (int64_t)ready) return true;
+            if (__hip_atomic_load(&hdr->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kWatchdogTicks) {
+                __hip_atomic_fetch_or(L.watchdog, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                return false;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    };
+    // One 16-byte vector of a row slot, zero past the row end (those LDS bytes are stale).
+    auto read_vec = [&](const char* slot, int v) __attribute__((always_inline)) -> V {
+        V xv = *reinterpret_cast<const V*>(slot + v * 1024 + lane * 16);
+        if constexpr (!FULL) {
+            if ((v * 64 + lane) * VEC >= dsc.ld) xv = V(0);
+        }
+        return xv;
+    };
+    auto to_pairs = [&](const V& xv, T2* out) __attribute__((always_inline)) {
+        float tmp[VEC];
+        unpack<S, float>(xv, tmp);
+#pragma unroll
+        for (int h = 0; h < H; ++h) out[h] = T2{tmp[2 * h], tmp[2 * h + 1]};
+    };
+
+    if (wave >= 2) {
+        // ---------------- Gram waves ----------------
+        const int gw = wave - 2;
+        // this lane's (k, i) after reduce32, as an offset into an 8x8 slot (-1: padding / odd lane)
+        const int j = ((lane >> 5) & 1) | (((lane >> 4) & 1) << 1) | (((lane >> 3) & 1) << 2) |
+                      (((lane >> 2) & 1) << 3) | (((lane >> 1) & 1) << 4);
+        int goff = -1;
+        {
+            int jj = 0;
+            for (int k = 1; k < kBlk; ++k)
+                for (int i = 0; i < k; ++i, ++jj)
+                    if (jj == j) goff = k * kBlk + i;
+            if (lane & 1) goff = -1;
+        }
+        unsigned ready = 0;
+        unsigned done = 0;
+        for (int64_t b = gw; b < nblk; b += 2) {
+            const int64_t t0 = b * kBlk;
+            const int64_t kk = (n - t0) < kBlk ? (n - t0) : kBlk;
+            if (!wait_ready(ready, t0 + kk, 4)) break;
+            const char* base = ring + (int)(t0 % R) * ROW_BYTES;
+            T2 acc[kPairs];
+#pragma unroll
+            for (int q = 0; q < kPairs; ++q) acc[q] = T2{0.0f, 0.0f};
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                T2 xc[kBlk][H];
+#pragma unroll
+                for (int k = 0; k < kBlk; ++k) to_pairs(read_vec(base + k * ROW_BYTES, v), xc[k]);
+                int q = 0;
+#pragma unroll
+                for (int k = 1; k < kBlk; ++k)
+#pragma unroll
+                    for (int i = 0; i < k; ++i, ++q)
+#pragma unroll
+                        for (int h = 0; h < H; ++h)
+                            acc[q] = __builtin_elementwise_fma(xc[k][h], xc[i][h], acc[q]);
+            }
+            float g[32];
+#pragma unroll
+            for (int q = 0; q < kPairs; ++q) g[q] = acc[q].x + acc[q].y;
+#pragma unroll
+            for (int q = kPairs; q < 32; ++q) g[q] = 0.0f;
+            const float val = reduce32(g, lane);
+            float* slot = gring + (int)(b % GS) * (kBlk * kBlk);
+            if (goff >= 0) slot[goff] = val;
+            ++done;
+            __hip_atomic_store(&ghdr->gdone[gw], done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        return;
+    }
+
+    // ---------------- chain wave ----------------
+    T2 w[E2];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const int base = (v * 64 + lane) * VEC;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            const int f = base + k;
+            const double wv = as_global(L.w_in)[f < d ? f : 0];
+            w[(v * VEC + k) / 2][(v * VEC + k) % 2] = f < d ? float(wv) : 0.0f;
+        }
+    }
+    const int krow = ((lane >> 5) & 1) | (((lane >> 4) & 1) << 1) | (((lane >> 3) & 1) << 2);
+    const bool loss_lane = (lane & 7) == 0;   // one copy of every row's loss
+    const float lam = float(kp.reg);
+    double loss_sum = 0.0;
+    float loss_blk = 0.0f;
+    int64_t count = 0;
+    unsigned ready = 0;
+
+    for (int64_t b = 0; b < nblk; ++b) {
+        const int64_t t0 = b * kBlk;
+        const int kk = (n - t0) < kBlk ? (int)(n - t0) : kBlk;
+        if (!wait_ready(ready, t0 + kk, 2)) break;
+        const char* base = ring + (int)(t0 % R) * ROW_BYTES;
+
+        // p_k = x_k . W (stale rows k >= kk give garbage in lanes that are never read)
+        T2 xk[KEEP ? kBlk : 1][KEEP ? E2 : 1];
+        float pk[kBlk];
+#pragma unroll
+        for (int k = 0; k < kBlk; ++k) {
+            T2 a0 = T2{0.0f, 0.0f}, a1 = T2{0.0f, 0.0f};
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                T2 xv[H];
+                to_pairs(read_vec(base + k * ROW_BYTES, v), xv);
+#pragma unroll
+                for (int h = 0; h < H; ++h) {
+                    const int e = v * H + h;
+                    if (e & 1) a1 = __builtin_elementwise_fma(xv[h], w[e], a1);
+                    else a0 = __builtin_elementwise_fma(xv[h], w[e], a0);
+                    if constexpr (KEEP) xk[k][e] = xv[h];
+                }
+            }
+            const T2 a = a0 + a1;
+            pk[k] = a.x + a.y;
+        }
+        // this lane's row: label and step
+        const int64_t tr = t0 + krow;
+        const f64x2 meta = *reinterpret_cast<const f64x2*>(
+            meta_ring + (int)((tr / kMetaRows) % MB) * kMetaBlockBytes + (int)(tr % kMetaRows) * 16);
+        const float yv = float(meta.x), sv = float(meta.y);
+        const float nsv = -sv;
+        float aux;
+        if constexpr (GRAD == G_LEAST_SQUARES) aux = sv * yv;
+        else if constexpr (GRAD == G_HINGE) aux = 2.0f * yv - 1.0f;
+        else aux = 0.0f;
+        const float alpha = 1.0f - sv * lam;      // SquaredL2 shrink of this lane's row
+        float z = reduce8(pk, lane);
+
+        // the block's Gram triangle (Gram wave b&1 publishes blocks in order)
+        {
+            const unsigned need = (unsigned)(b >> 1) + 1;
+            unsigned* gd = &ghdr->gdone[b & 1];
+            if (__hip_atomic_load(gd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+                const uint64_t tw = __builtin_amdgcn_s_memrealtime();
+                bool ok = true;
+                while (__hip_atomic_load(gd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+                    if (__builtin_amdgcn_s_memrealtime() - tw > kWatchdogTicks) {
+                        __hip_atomic_fetch_or(L.watchdog, 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        ok = false;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                if (!ok) break;
+            }
+        }
+        const float* grow = gring + (int)(b % GS) * (kBlk * kBlk) + krow * kBlk;
+        const f32x4 g0 = *reinterpret_cast<const f32x4*>(grow);
+        const f32x4 g1 = *reinterpret_cast<const f32x4*>(grow + 4);
+        const float G[kBlk] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+        if constexpr (KEEP) {
+            // rows, labels, steps and the Gram row are in registers: free the slots
+            __hip_atomic_store(&hdr->consumed, (unsigned)(t0 + kk), __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+
+        // the scalar recurrence: c_i from z_i, then every later row's dot moves by c_i G[k][i]
+        // (SquaredL2 also shrinks the finished rows' z: zf keeps z_k for the loss)
+        float c[kBlk], al[kBlk];
+        float zf = z;
+        if (kk == kBlk) {
+#pragma unroll
+            for (int i = 0; i < kBlk; ++i) {
+                c[i] = readlane_f(coef<GRAD>(z, yv, sv, nsv, aux), row_lane(i));
+                if constexpr (UPD == U_SQUARED_L2) {
+                    if (krow == i) zf = z;
+                    al[i] = readlane_f(alpha, row_lane(i));
+                    if (i + 1 < kBlk) z = __builtin_fmaf(c[i], G[i], al[i] * z);
+                } else {
+                    if (i + 1 < kBlk) z = __builtin_fmaf(c[i], G[i], z);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < kBlk; ++i) {
+                c[i] = 0.0f;
+                al[i] = 1.0f;
+                if (i < kk) {
+                    c[i] = readlane_f(coef<GRAD>(z, yv, sv, nsv, aux), row_lane(i));
+                    if constexpr (UPD == U_SQUARED_L2) {
+                        if (krow == i) zf = z;
+                        al[i] = readlane_f(alpha, row_lane(i));
+                        z = __builtin_fmaf(c[i], G[i], al[i] * z);
+                    } else {
+                        z = __builtin_fmaf(c[i], G[i], z);
+                    }
+                }
+            }
+        }
+        // z (zf for SquaredL2) now holds z_k in every lane of row k
+        if constexpr (UPD != U_SQUARED_L2) zf = z;
+        {
+            const float l = row_loss<GRAD>(zf, yv, aux);
+            if (loss_lane && krow < kk) loss_blk += l;
+            if ((b & 3) == 3) { loss_sum += double(loss_blk); loss_blk = 0.0f; }
+        }
+        count += kk;
+
+        // W <- a_i W + c_i x_i, i = 0..kk-1, in sample order
+#pragma unroll
+        for (int i = 0; i < kBlk; ++i) {
+            if (kk == kBlk || i < kk) {
+                const T2 ci = T2{c[i], c[i]};
+                if constexpr (KEEP) {
+#pragma unroll
+                    for (int e = 0; e < E2; ++e) {
+                        if constexpr (UPD == U_SQUARED_L2)
+                            w[e] = __builtin_elementwise_fma(ci, xk[i][e], w[e] * T2{al[i], al[i]});
+                        else
+                            w[e] = __builtin_elementwise_fma(ci, xk[i][e], w[e]);
+                    }
+                } else {
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) {
+                        T2 xv[H];
+                        to_pairs(read_vec(base + i * ROW_BYTES, v), xv);
+#pragma unroll
+                        for (int h = 0; h < H; ++h) {
+                            const int e = v * H + h;
+                            if constexpr (UPD == U_SQUARED_L2)
+                                w[e] = __builtin_elementwise_fma(ci, xv[h], w[e] * T2{al[i], al[i]});
+                            else
+                                w[e] = __builtin_elementwise_fma(ci, xv[h], w[e]);
+                        }
+                    }
+                }
+            }
+        }
+        if constexpr (!KEEP) {
+            __hip_atomic_store(&hdr->consumed, (unsigned)(t0 + kk), __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    // a wave that stopped early leaves the others blocked on it: wake them
+    __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    loss_sum += double(loss_blk);
+    // the loss partials of the 8 loss lanes
+    {
+        double ls = loss_sum;
+        ls = wave_sum(ls);
+        loss_sum = ls;
+    }
+    if constexpr (GRAD == G_LEAST_SQUARES) loss_sum = loss_sum / 2.0;
+
+    // regVal of the chain's last update (PSGD.scala:257; 0.0 if no sample, :247)
+    double rv = 0.0;
+    if constexpr (UPD == U_SQUARED_L2) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int e = 0; e < E2; ++e) acc += w[e].x * w[e].x + w[e].y * w[e].y;
+        acc = wave_sum(acc);
+        if (count > 0) {
+            const double nrm = sqrt(double(acc));
+            rv = 0.5 * kp.reg * nrm * nrm;
+        }
+    }
+
+    double* wo = L.w_out + (int64_t)chain * d;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const int base = (v * 64 + lane) * VEC;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k)
+            if (base + k < d) wo[base + k] = double(w[(v * VEC + k) / 2][(v * VEC + k) % 2]);
+    }
+    if (lane == 0) {
+        L.rv[chain] = rv;
+        L.loss[chain] = loss_sum;
+        L.cnt[chain] = count;
+        L.cnt_d[chain] = double(count);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Launcher.
+// ------------------------------------------------------------------------------------------
+template <typename S, int GRAD, int UPD, int NV>
+static int launch_block(const ChainLaunch& L, const KParams& kp, bool full, size_t lds, hipStream_t st) {
+    constexpr int ROW = NV * 1024;
+    const size_t budget = lds > 0 ? lds : (size_t)64 * 1024;
+    const size_t fixed = sizeof(RingHeader) + sizeof(GramHeader);
+    int D = 56 / NV;
+    if (D > 32) D = 32;
+    int R = 0, MB = 0, GS = 0;
+    auto bytes_for = [&](int r) {
+        const int mb = (r + kMetaRows - 1) / kMetaRows + 2;
+        const int gs = r / kBlk + 1;
+        return fixed + (size_t)mb * kMetaBlockBytes + (size_t)gs * kBlk * kBlk * 4 + (size_t)r * ROW;
+    };
+    for (;;) {
+        R = (int)((budget - fixed) / ROW) / kBlk * kBlk;
+        while (R > 0 && bytes_for(R) > budget) R -= kBlk;
+        if (R >= D + kBlk || D == 1) break;
+        D = D > 2 ? D / 2 : 1;
+    }
+    if (R < D + kBlk) return (int)hipErrorInvalidValue;  // LDS budget too small for this d
+    MB = (R + kMetaRows - 1) / kMetaRows + 2;
+    GS = R / kBlk + 1;
+    RingGeom g{R, MB, D, GS};
+    const size_t bytes = bytes_for(R);
+    if (full) {
+        auto k = chain_block<S, GRAD, UPD, NV, true>;
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(256), bytes, st, L, kp, g);
+    } else {
+        auto k = chain_block<S, GRAD, UPD, NV, false>;
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(256), bytes, st, L, kp, g);
+    }
+    return (int)hipGetLastError();
+}
+
+template <typename S, int GRAD, int UPD>
+static int block_nv(const ChainLaunch& L, const KParams& kp, int64_t min_ld, int64_t max_ld,
+                    size_t lds, hipStream_t st, int* variant) {
+    constexpr int VEC = 16 / sizeof(S);
+    int nv = 1;
+    while (nv * 64 * VEC < max_ld) nv *= 2;
+    const bool full = min_ld >= (int64_t)nv * 64 * VEC;
+    if (variant) *variant = 300 + nv;
+    switch (nv) {
+    case 1: return launch_block<S, GRAD, UPD, 1>(L, kp, full, lds, st);
+    case 2: return launch_block<S, GRAD, UPD, 2>(L, kp, full, lds, st);
+    case 4: return launch_block<S, GRAD, UPD, 4>(L, kp, full, lds, st);
+    case 8: return launch_block<S, GRAD, UPD, 8>(L, kp, full, lds, st);
+    default: return -3;
+    }
+}
+
+template <typename S, int GRAD>
+static int block_upd(const ChainLaunch& L, const KParams& kp, int upd, int64_t min_ld,
+                     int64_t max_ld, size_t lds, hipStream_t st, int* variant) {
+    if (upd == U_SIMPLE) return block_nv<S, GRAD, U_SIMPLE>(L, kp, min_ld, max_ld, lds, st, variant);
+    if (upd == U_SQUARED_L2) return block_nv<S, GRAD, U_SQUARED_L2>(L, kp, min_ld, max_ld, lds, st, variant);
+    return -3;
+}
+
+template <typename S>
+static int block_grad(const ChainLaunch& L, const KParams& kp, int grad, int upd, int64_t min_ld,
+                      int64_t max_ld, size_t lds, hipStream_t st, int* variant) {
+    switch (grad) {
+    case G_LOGISTIC: return block_upd<S, G_LOGISTIC>(L, kp, upd, min_ld, max_ld, lds, st, variant);
+    case G_LEAST_SQUARES: return block_upd<S, G_LEAST_SQUARES>(L, kp, upd, min_ld, max_ld, lds, st, variant);
+    case G_HINGE: return block_upd<S, G_HINGE>(L, kp, upd, min_ld, max_ld, lds, st, variant);
+    default: return -3;
+    }
+}
+
+bool block_path_applies(int layout, int compute, int updater, bool check_conv, int storage,
+                        int64_t max_ld) {
+    const int vec = storage == 1 ? 4 : 2;
+    return layout == kDense && compute == 1 && !check_conv &&
+           (updater == U_SIMPLE || updater == U_SQUARED_L2) && max_ld <= 8 * 64 * vec;
+}
+
+int launch_block_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
+                        int updater, int64_t min_ld, int64_t max_ld, int lds_spread,
+                        hipStream_t stream, int* kernel_variant) {
+    if (kp.n_chains <= 0) return 0;
+    const size_t lds = (size_t)(lds_spread > 0 ? lds_spread : 0);
+    if (storage == 1)
+        return block_grad<float>(L, kp, gradient, updater, min_ld, max_ld, lds, stream, kernel_variant);
+    return block_grad<double>(L, kp, gradient, updater, min_ld, max_ld, lds, stream, kernel_variant);
+}
+
+}  // namespace psgd

@@ -91,6 +91,9 @@ struct psgd_ctx {
     double steps_value = NAN;
     int64_t steps_n = 0;
     int32_t last_variant = 0;
+    // HIP events around the last chain-kernel launch (psgd_ctx_last_chain_ms)
+    hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+    bool ev_recorded = false;
 };
 
 namespace {
@@ -263,6 +266,8 @@ int32_t psgd_ctx_destroy(psgd_ctx* ctx) {
                           &ctx->cnt_d, &ctx->cnt, &ctx->steps, &ctx->partial, &ctx->tmp,
                           &ctx->watchdog})
             b->release();
+        if (ctx->ev_begin) hipEventDestroy(ctx->ev_begin);
+        if (ctx->ev_end) hipEventDestroy(ctx->ev_end);
         hipStreamDestroy(ctx->stream);
     }
     delete ctx;
@@ -486,10 +491,17 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         HIP_TRY(hipMemsetAsync(L.cnt_d, 0, P * sizeof(double), st));
         HIP_TRY(hipMemsetAsync(L.cnt, 0, P * sizeof(int64_t), st));
     } else {
+        if (!ctx->ev_begin) {
+            HIP_TRY(hipEventCreate(&ctx->ev_begin));
+            HIP_TRY(hipEventCreate(&ctx->ev_end));
+        }
+        HIP_TRY(hipEventRecord(ctx->ev_begin, st));
         int e = psgd::launch_chains(L, kp, layout, first.dtype == PSGD_F32 ? 1 : 0,
                                     params->compute_dtype == PSGD_F32 ? 1 : 0, params->gradient,
                                     params->updater, conv, min_ld, max_ld,
                                     lds_spread_bytes(ctx, (size_t)P), st, &ctx->last_variant);
+        HIP_TRY(hipEventRecord(ctx->ev_end, st));
+        ctx->ev_recorded = (e == 0);
         if (e == -2) return fail(PSGD_EUNSUPPORTED, "this gradient/updater/layout combination is not built");
         if (e) return fail(PSGD_EDEVICE, std::string("chain kernel launch failed: ") +
                                              hipGetErrorString((hipError_t)e));
@@ -611,5 +623,16 @@ int32_t psgd_initial_regval(psgd_ctx* ctx, const psgd_params* params, int32_t d,
 }
 
 int32_t psgd_ctx_last_kernel(psgd_ctx* ctx) { return ctx ? ctx->last_variant : 0; }
+
+int32_t psgd_ctx_last_chain_ms(psgd_ctx* ctx, double* ms_out) {
+    if (!ctx || !ms_out) return fail(PSGD_EINVAL, "ctx/ms_out is null");
+    if (!ctx->ev_recorded) return fail(PSGD_ESTATE, "no chain kernel has been launched");
+    DeviceGuard g(ctx->device);
+    HIP_TRY(hipEventSynchronize(ctx->ev_end));
+    float ms = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&ms, ctx->ev_begin, ctx->ev_end));
+    *ms_out = ms;
+    return PSGD_OK;
+}
 
 }  // extern "C"

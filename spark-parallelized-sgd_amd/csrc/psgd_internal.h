@@ -47,6 +47,13 @@ struct ChainLaunch {
 int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int storage, int compute,
                   int gradient, int updater, bool check_conv, int64_t min_ld, int64_t max_ld,
                   int lds_spread, hipStream_t stream, int* kernel_variant);
+// The blocked fp32 kernel (psgd_block.hip): dense rows, Simple/SquaredL2, no per-sample
+// convergence test. launch_block_chains returns -3 when it does not apply.
+bool block_path_applies(int layout, int compute, int updater, bool check_conv, int storage,
+                        int64_t max_ld);
+int launch_block_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
+                        int updater, int64_t min_ld, int64_t max_ld, int lds_spread,
+                        hipStream_t stream, int* kernel_variant);
 int launch_fold(const double* w, int64_t w_stride, const double* rv, const double* loss,
                 const double* cnt, int64_t s_stride, int n, int d, double* out,
                 const int* watchdog, hipStream_t stream);

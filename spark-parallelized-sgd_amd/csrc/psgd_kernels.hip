@@ -19,275 +19,11 @@
 // the MLlib gradient), L2 scaling w_i * (1 - s*lambda) before it. Only the dot product and the
 // norms are reassociated (wave tree instead of the F2J left fold), so fp64 mode agrees with the
 // reference to rounding, not bitwise.
-#include "psgd_internal.h"
+#include "psgd_device.h"
 
-#include <hip/hip_runtime.h>
-#include <math.h>
-
-#include <utility>
+#include <stdlib.h>
 
 namespace psgd {
-
-enum { G_LOGISTIC = 0, G_LEAST_SQUARES = 1, G_HINGE = 2 };
-enum { U_SIMPLE = 0, U_SQUARED_L2 = 1, U_L1 = 2, U_ADAGRAD = 3, U_ADAM = 4 };
-
-// ------------------------------------------------------------------------------------------
-// Wave-wide all-reduce. Every step adds a lane's value to its partner's (partners swap), so
-// each lane computes the same two operands in the same order and ends with the same bits.
-// ------------------------------------------------------------------------------------------
-template <int CTRL>
-__device__ __forceinline__ float dpp_mov(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-template <int CTRL>
-__device__ __forceinline__ double dpp_mov(double v) {
-    long long b = __double_as_longlong(v);
-    int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, 0xF, 0xF, false);
-    int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
-// v_permlane16_swap / v_permlane32_swap (gfx950): with both operands = v, the pair returned
-// holds {value of the even partner, value of the odd partner} in every lane.
-__device__ __forceinline__ float swap_sum16(float v) {
-    auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return __uint_as_float(p[0]) + __uint_as_float(p[1]);
-}
-__device__ __forceinline__ float swap_sum32(float v) {
-    auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return __uint_as_float(p[0]) + __uint_as_float(p[1]);
-}
-__device__ __forceinline__ double swap_sum16(double v) {
-    unsigned long long b = (unsigned long long)__double_as_longlong(v);
-    unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32);
-    auto pl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-    auto ph = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-    double e = __longlong_as_double((long long)(((unsigned long long)ph[0] << 32) | pl[0]));
-    double o = __longlong_as_double((long long)(((unsigned long long)ph[1] << 32) | pl[1]));
-    return e + o;
-}
-__device__ __forceinline__ double swap_sum32(double v) {
-    unsigned long long b = (unsigned long long)__double_as_longlong(v);
-    unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32);
-    auto pl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-    auto ph = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-    double e = __longlong_as_double((long long)(((unsigned long long)ph[0] << 32) | pl[0]));
-    double o = __longlong_as_double((long long)(((unsigned long long)ph[1] << 32) | pl[1]));
-    return e + o;
-}
-
-template <typename T>
-__device__ __forceinline__ T wave_sum(T v) {
-    v = v + dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
-    v = v + dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
-    v = v + dpp_mov<0x141>(v);  // row_half_mirror
-    v = v + dpp_mov<0x140>(v);  // row_mirror
-    v = swap_sum16(v);
-    v = swap_sum32(v);
-    return v;
-}
-
-// Wave sum delivered as a wave-uniform value: four DPP row steps, then row_bcast:15 / :31 fold
-// the four row sums into lane 63 ((r3 + r2) + (r1 + r0)), which v_readlane broadcasts. Two
-// fewer instructions than the swap form and the result lands in SGPRs for the scalar math.
-template <int CTRL, int ROWS>
-__device__ __forceinline__ float dpp_mov_rows(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWS, 0xF, false));
-}
-template <int CTRL, int ROWS>
-__device__ __forceinline__ double dpp_mov_rows(double v) {
-    long long b = __double_as_longlong(v);
-    int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, ROWS, 0xF, false);
-    int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWS, 0xF, false);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-__device__ __forceinline__ float readlane63(float v) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
-}
-__device__ __forceinline__ double readlane63(double v) {
-    long long b = __double_as_longlong(v);
-    int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), 63);
-    int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-template <typename T>
-__device__ __forceinline__ T wave_sum_uniform(T v) {
-    v = v + dpp_mov<0xB1>(v);            // quad_perm [1,0,3,2]
-    v = v + dpp_mov<0x4E>(v);            // quad_perm [2,3,0,1]
-    v = v + dpp_mov<0x141>(v);           // row_half_mirror
-    v = v + dpp_mov<0x140>(v);           // row_mirror: every lane holds its row's sum
-    v = v + dpp_mov_rows<0x142, 0xA>(v); // row_bcast:15 -> rows 1, 3 hold r0+r1, r2+r3
-    v = v + dpp_mov_rows<0x143, 0xC>(v); // row_bcast:31 -> row 3 holds the total
-    return readlane63(v);
-}
-
-// Two independent sums reduced together (ILP for the convergence terms).
-template <typename T>
-__device__ __forceinline__ void wave_sum2(T& a, T& b) {
-    a = a + dpp_mov<0xB1>(a);  b = b + dpp_mov<0xB1>(b);
-    a = a + dpp_mov<0x4E>(a);  b = b + dpp_mov<0x4E>(b);
-    a = a + dpp_mov<0x141>(a); b = b + dpp_mov<0x141>(b);
-    a = a + dpp_mov<0x140>(a); b = b + dpp_mov<0x140>(b);
-    a = swap_sum16(a);         b = swap_sum16(b);
-    a = swap_sum32(a);         b = swap_sum32(b);
-}
-
-__device__ __forceinline__ double readlane_d(double v, int lane) {
-    long long b = __double_as_longlong(v);
-    int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
-    int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
-// Global-address-space views: loads through them are global_load_* (in-order vmcnt) instead of
-// flat_load_* (which also count on lgkmcnt and force full drains before every use).
-template <typename T>
-using gptr = const T __attribute__((address_space(1)))*;
-template <typename T>
-using gmut = T __attribute__((address_space(1)))*;
-template <typename T>
-__device__ __forceinline__ gptr<T> as_global(const T* p) { return (gptr<T>)(p); }
-template <typename T>
-__device__ __forceinline__ gmut<T> as_global_mut(T* p) { return (gmut<T>)(p); }
-
-// ------------------------------------------------------------------------------------------
-// Scalar math per precision.
-// ------------------------------------------------------------------------------------------
-__device__ __forceinline__ double m_exp(double x) { return exp(x); }
-__device__ __forceinline__ float m_exp(float x) { return expf(x); }
-__device__ __forceinline__ double m_log1p(double x) { return log1p(x); }
-__device__ __forceinline__ float m_log1p(float x) { return log1pf(x); }
-__device__ __forceinline__ double m_sqrt(double x) { return sqrt(x); }
-__device__ __forceinline__ double m_fabs(double x) { return __builtin_fabs(x); }
-__device__ __forceinline__ float m_fabs(float x) { return __builtin_fabsf(x); }
-__device__ __forceinline__ float m_sqrt(float x) { return sqrtf(x); }
-__device__ __forceinline__ double m_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
-__device__ __forceinline__ float m_fma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
-
-// java.lang.Math.max(a, b): NaN if either is NaN.
-template <typename T>
-__device__ __forceinline__ T jmax(T a, T b) {
-    return (a != a) ? a : ((b != b) ? b : (a >= b ? a : b));
-}
-// java.lang.Math.signum
-template <typename T>
-__device__ __forceinline__ T jsignum(T x) {
-    return (x != x || x == T(0)) ? x : (x > T(0) ? T(1) : T(-1));
-}
-
-// [ext] MLlib 1.6.1 MLUtils.log1pExp
-template <typename T>
-__device__ __forceinline__ T log1p_exp(T x) {
-    return x > T(0) ? x + m_log1p(m_exp(-x)) : m_log1p(m_exp(x));
-}
-
-// [ext] MLlib 1.6.1 Gradient.compute: the gradient is mult * x (Logistic: axpy(mult, x, 0);
-// LeastSquares: scal(diff, x.copy); Hinge: scal(-labelScaled, x.copy) or the empty vector,
-// which adds nothing -- mult = 0 gives the same weights). Returns loss.
-template <int GRAD, typename T>
-__device__ __forceinline__ T gradient_scalar(T z, T y, T& mult) {
-    if constexpr (GRAD == G_LOGISTIC) {
-        T margin = -z;                                    // -1.0 * dot(data, weights)
-        mult = (T(1) / (T(1) + m_exp(margin))) - y;
-        T l = log1p_exp(margin);
-        return y > T(0) ? l : l - margin;
-    } else if constexpr (GRAD == G_LEAST_SQUARES) {
-        T diff = z - y;
-        mult = diff;
-        return diff * diff / T(2);
-    } else {
-        T ls = T(2) * y - T(1);
-        T lz = ls * z;
-        bool on = T(1) > lz;
-        mult = on ? -ls : T(0);
-        return on ? T(1) - lz : T(0);
-    }
-}
-
-template <int... Is, typename F>
-__device__ __forceinline__ void static_for_impl(std::integer_sequence<int, Is...>, F&& f) {
-    (f(std::integral_constant<int, Is>{}), ...);
-}
-// Calls f(std::integral_constant<int, i>) for i = 0..N-1: a guaranteed compile-time unroll.
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-    static_for_impl(std::make_integer_sequence<int, N>{}, f);
-}
-
-template <typename S> struct Vec16;
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef double f64x2 __attribute__((ext_vector_type(2)));
-template <> struct Vec16<float> { using type = f32x4; static constexpr int N = 4; };
-template <> struct Vec16<double> { using type = f64x2; static constexpr int N = 2; };
-
-template <typename S, typename T>
-__device__ __forceinline__ void unpack(const typename Vec16<S>::type& v, T* out) {
-    if constexpr (Vec16<S>::N == 4) {
-        out[0] = T(v.x); out[1] = T(v.y); out[2] = T(v.z); out[3] = T(v.w);
-    } else {
-        out[0] = T(v.x); out[1] = T(v.y);
-    }
-}
-
-// ------------------------------------------------------------------------------------------
-// chain_dense: dense rows, weights in VGPRs, rows streamed through an LDS ring.
-//
-// One workgroup = one chain = two waves on two SIMDs:
-//   wave 1 (loader)  streams the partition's rows, in iterator order, into an R-slot LDS ring
-//                    with global_load_lds (LDS DMA, 1 KiB per instruction, up to ~60 KiB in
-//                    flight), plus each row's label and stepSize/sqrt(j) (the "meta" bytes), and
-//                    publishes `ready` = number of rows that have landed;
-//   wave 0 (compute) owns the weights in registers and runs the sequential chain:
-//                    lane l, vector v (0..NV-1) owns features (v*64 + l)*VEC .. +VEC-1, so a
-//                    row slot is read with NV ds_read_b128 per lane; it publishes `consumed`.
-// Only the loader issues VMEM, so the compute wave never waits on vmcnt; the loader's LDS
-// accesses are inline asm so that the compiler does not drain its DMA before them.
-// ------------------------------------------------------------------------------------------
-struct RingHeader {
-    unsigned ready;     // rows landed in the ring (loader -> compute)
-    unsigned consumed;  // rows whose slot may be refilled (compute -> loader)
-    unsigned stop;      // compute wave left the chain early (per-sample convergence break)
-    unsigned pad;
-};
-// Labels and steps travel in 256-byte meta blocks, one per 16 rows: {y, stepSize/sqrt(j)} x 16.
-constexpr int kMetaRows = 16;
-constexpr int kMetaBlockBytes = 256;
-// s_memrealtime runs at 100 MHz: a wave that sees no progress from its partner for 4 s sets the
-// launch's watchdog word and leaves (the host then raises instead of hanging).
-constexpr uint64_t kWatchdogTicks = 400000000ull;
-
-// s_waitcnt vmcnt(k) for a runtime k (the immediate must be a constant).
-__device__ __forceinline__ void wait_vmcnt_le(int k) {
-#define PSGD_VMCNT_CASE(K) case K: asm volatile("s_waitcnt vmcnt(" #K ")" ::: "memory"); break;
-    switch (k) {
-        PSGD_VMCNT_CASE(0) PSGD_VMCNT_CASE(1) PSGD_VMCNT_CASE(2) PSGD_VMCNT_CASE(3)
-        PSGD_VMCNT_CASE(4) PSGD_VMCNT_CASE(5) PSGD_VMCNT_CASE(6) PSGD_VMCNT_CASE(7)
-        PSGD_VMCNT_CASE(8) PSGD_VMCNT_CASE(10) PSGD_VMCNT_CASE(12) PSGD_VMCNT_CASE(14)
-        PSGD_VMCNT_CASE(16) PSGD_VMCNT_CASE(20) PSGD_VMCNT_CASE(24) PSGD_VMCNT_CASE(28)
-        PSGD_VMCNT_CASE(32) PSGD_VMCNT_CASE(36) PSGD_VMCNT_CASE(40) PSGD_VMCNT_CASE(44)
-        PSGD_VMCNT_CASE(48) PSGD_VMCNT_CASE(52) PSGD_VMCNT_CASE(56) PSGD_VMCNT_CASE(60)
-        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    }
-#undef PSGD_VMCNT_CASE
-}
-
-// Ring geometry chosen by the launcher (psgd_kernels.hip, launch_reg).
-struct RingGeom {
-    int rows;         // R row slots
-    int meta_blocks;  // MB meta blocks (16 rows each)
-    int depth;        // D: rows the loader keeps in flight past the oldest unpublished one
-};
-
-__device__ __forceinline__ unsigned lds_load_u32_asm(const unsigned* p) {
-    unsigned v;
-    const unsigned addr = (unsigned)(uintptr_t)p;
-    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
-    return v;
-}
-__device__ __forceinline__ void lds_store_u32_asm(unsigned* p, unsigned v) {
-    const unsigned addr = (unsigned)(uintptr_t)p;
-    asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : : "v"(addr), "v"(v) : "memory");
-}
 
 template <typename S, typename T, int GRAD, int UPD, bool CONV, int NV, bool FULL>
 __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, RingGeom geom) {
@@ -318,62 +54,7 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, Ri
     __syncthreads();
 
     if (wave == 1) {
-        // ---------------- loader ----------------
-        const int D = geom.depth;
-        const S* X = reinterpret_cast<const S*>(dsc.x);
-        const int64_t ld = dsc.ld;
-        // meta DMA lane l: row 16k + l/4, dword l%4 of {y lo, y hi, step lo, step hi}
-        const unsigned* msrc = reinterpret_cast<const unsigned*>((lane & 2) ? L.steps : dsc.y) + (lane & 1);
-        const int mrow = lane >> 2;
-        unsigned consumed = 0;
-        int64_t published = 0;
-        int slot = 0, mslot = 0;
-        for (int64_t t = 0; t < n; ++t) {
-            if (t >= (int64_t)consumed + R) {
-                // ring full: wait for the compute wave to free the slot of row t - R
-                // (R - D >= 8 keeps enough rows published that this cannot deadlock)
-                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-                for (;;) {
-                    consumed = lds_load_u32_asm(&hdr->consumed);
-                    if (t < (int64_t)consumed + R) break;
-                    if (lds_load_u32_asm(&hdr->stop)) goto drain;
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > kWatchdogTicks) {
-                        __hip_atomic_fetch_or(L.watchdog, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        goto drain;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-            }
-            if ((t & (kMetaRows - 1)) == 0) {
-                int64_t r = t + mrow;
-                if (r >= n) r = n - 1;
-                __builtin_amdgcn_global_load_lds(
-                    (const void*)(as_global(msrc + 2 * r)),
-                    (__attribute__((address_space(3))) void*)(meta_ring + mslot * kMetaBlockBytes), 4, 0, 0);
-                if (++mslot == MB) mslot = 0;
-            }
-            {
-                char* dst = ring + slot * ROW_BYTES;
-                const V* row = reinterpret_cast<const V*>(X + t * ld);
-#pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    if (FULL || (v * 64 + lane) * VEC < ld)
-                        __builtin_amdgcn_global_load_lds(
-                            (const void*)(as_global(row + v * 64 + lane)),
-                            (__attribute__((address_space(3))) void*)(dst + v * 1024), 16, 0, 0);
-                }
-            }
-            if (++slot == R) slot = 0;
-            if (t >= D) {
-                // all but the newest D rows' instructions are done: row t - D has landed
-                wait_vmcnt_le(D * NV);
-                published = t - D + 1;
-                lds_store_u32_asm(&hdr->ready, (unsigned)published);
-            }
-        }
-    drain:
-        asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
-        lds_store_u32_asm(&hdr->ready, (unsigned)n);
+        ring_loader<S, NV, FULL>(L, dsc, hdr, meta_ring, ring, geom, lane);
         return;
     }
 
@@ -793,6 +474,7 @@ __global__ void fold_kernel(const double* __restrict__ w, int64_t w_stride,
     if (i < d) {
         double acc = w[i];
         double c1 = cnt[0];
+#pragma unroll 16
         for (int p = 1; p < n; ++p) {
             const double c2 = cnt[p * s_stride];
             acc = (acc * c1 + w[p * w_stride + i] * c2) / (c1 + c2);
@@ -871,7 +553,7 @@ static int launch_reg(const ChainLaunch& L, const KParams& kp, bool full, size_t
         D = D > 2 ? D / 2 : 1;
     }
     if (R < D + 3) return (int)hipErrorInvalidValue;  // LDS budget too small for this d
-    RingGeom g{R, MB, D};
+    RingGeom g{R, MB, D, 0};
     const size_t bytes = sizeof(RingHeader) + (size_t)MB * kMetaBlockBytes + (size_t)R * ROW;
     if (full) {
         auto k = chain_dense<S, T, GRAD, UPD, CONV, NV, true>;
@@ -962,6 +644,14 @@ int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int stora
                   int gradient, int updater, bool check_conv, int64_t min_ld, int64_t max_ld,
                   int lds_spread, hipStream_t stream, int* kernel_variant) {
     if (kp.n_chains <= 0) return 0;
+    // PSGD_PER_SAMPLE=1 keeps fp32 mode on the per-sample kernel (A/B measurements)
+    static const bool per_sample = [] {
+        const char* e = getenv("PSGD_PER_SAMPLE");
+        return e && *e && *e != '0';
+    }();
+    if (!per_sample && block_path_applies(layout, compute, updater, check_conv, storage, max_ld))
+        return launch_block_chains(L, kp, storage, gradient, updater, min_ld, max_ld, lds_spread,
+                                   stream, kernel_variant);
     const size_t lds = (size_t)(lds_spread > 0 ? lds_spread : 0);
     if (storage == 1)
         return dispatch_grad<float>(L, kp, layout, compute, gradient, updater, check_conv, min_ld,

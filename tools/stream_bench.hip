@@ -1,0 +1,130 @@
+// stream_bench.hip -- ceilings for the chain kernels' row stream on MI355X (diagnostic tool, not
+// part of the product). Every workgroup streams its own contiguous partition of `rows` rows of
+// `rowbytes` bytes, the chain kernels' access pattern (one partition per CU):
+//   plain    : 4 waves per workgroup, global_load_dwordx4 into registers, rows split over waves
+//   plain1   : 1 wave per workgroup, global_load_dwordx4, 8 rows in flight
+//   ldsdma   : ring_loader (the chain kernels' loader) + a consumer wave that hands every slot
+//              straight back (no compute): the loader/handshake ceiling
+// Usage: stream_bench <rows per partition> <partitions> <R ring rows> <D depth>
+#include "../spark-parallelized-sgd_amd/csrc/psgd_device.h"
+
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+using namespace psgd;
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
+
+__global__ __launch_bounds__(256) void plain(const float4* __restrict__ X, int64_t rows_per, int nv,
+                                             float* out) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const float4* base = X + (int64_t)blockIdx.x * rows_per * nv * 64;
+    float4 acc = {0, 0, 0, 0};
+    for (int64_t r = wave; r < rows_per; r += 4) {
+        for (int v = 0; v < nv; ++v) {
+            float4 x = base[(r * nv + v) * 64 + lane];
+            acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
+        }
+    }
+    if (acc.x == 1234.5f) out[0] = acc.y + acc.z + acc.w;
+}
+
+__global__ __launch_bounds__(64) void plain1(const float4* __restrict__ X, int64_t rows_per, int nv,
+                                             float* out) {
+    const int lane = threadIdx.x & 63;
+    const float4* base = X + (int64_t)blockIdx.x * rows_per * nv * 64;
+    float4 acc = {0, 0, 0, 0};
+    const int64_t total = rows_per * nv;
+    int64_t i = 0;
+    for (; i + 16 <= total; i += 16) {
+        float4 x[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x[k] = base[(i + k) * 64 + lane];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) { acc.x += x[k].x; acc.y += x[k].y; acc.z += x[k].z; acc.w += x[k].w; }
+    }
+    if (acc.x == 1234.5f) out[0] = acc.y + acc.z + acc.w;
+}
+
+template <int NV>
+__global__ __launch_bounds__(128) void ldsdma(ChainLaunch L, RingGeom geom) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    RingHeader* hdr = reinterpret_cast<RingHeader*>(smem);
+    char* meta_ring = smem + sizeof(RingHeader);
+    char* ring = meta_ring + geom.meta_blocks * kMetaBlockBytes;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const ChainDesc dsc = L.descs[blockIdx.x];
+    if (threadIdx.x == 0) { hdr->ready = 0; hdr->consumed = 0; hdr->stop = 0; }
+    __syncthreads();
+    if (wave == 1) {
+        ring_loader<float, NV, true>(L, dsc, hdr, meta_ring, ring, geom, lane);
+        return;
+    }
+    const int64_t n = dsc.n_rows;
+    unsigned ready = 0;
+    while ((int64_t)ready < n) {
+        ready = __hip_atomic_load(&hdr->ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(&hdr->consumed, ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+int main(int argc, char** argv) {
+    const int64_t rows = argc > 1 ? atoll(argv[1]) : 39062;
+    const int P = argc > 2 ? atoi(argv[2]) : 256;
+    const int R = argc > 3 ? atoi(argv[3]) : 64;
+    const int D = argc > 4 ? atoi(argv[4]) : 28;
+    const int nv = 2;  // d = 512 f32
+    const int64_t rowbytes = nv * 1024;
+    const size_t bytes = (size_t)rows * P * rowbytes;
+    void* X;
+    CK(hipMalloc(&X, bytes));
+    CK(hipMemset(X, 0, bytes));
+    double* y; double* steps; int* wd; float* out;
+    CK(hipMalloc(&y, rows * P * 8)); CK(hipMemset(y, 0, rows * P * 8));
+    CK(hipMalloc(&steps, rows * 8)); CK(hipMemset(steps, 0, rows * 8));
+    CK(hipMalloc(&wd, 4)); CK(hipMemset(wd, 0, 4));
+    CK(hipMalloc(&out, 4));
+    ChainDesc* h = (ChainDesc*)calloc(P, sizeof(ChainDesc));
+    for (int p = 0; p < P; ++p) {
+        h[p].x = (char*)X + (size_t)p * rows * rowbytes;
+        h[p].y = y + (size_t)p * rows;
+        h[p].n_rows = rows;
+        h[p].ld = nv * 256;
+    }
+    ChainDesc* dd;
+    CK(hipMalloc(&dd, P * sizeof(ChainDesc)));
+    CK(hipMemcpy(dd, h, P * sizeof(ChainDesc), hipMemcpyHostToDevice));
+    ChainLaunch L{};
+    L.descs = dd; L.steps = steps; L.watchdog = wd;
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+    auto timeit = [&](const char* name, auto launch) {
+        launch();
+        CK(hipDeviceSynchronize());
+        float best = 1e30f;
+        for (int it = 0; it < 3; ++it) {
+            CK(hipEventRecord(a));
+            launch();
+            CK(hipEventRecord(b));
+            CK(hipEventSynchronize(b));
+            float ms; CK(hipEventElapsedTime(&ms, a, b));
+            if (ms < best) best = ms;
+        }
+        printf("%-10s %8.3f ms  %8.1f GB/s  (%.1f ns/row/CU)\n", name, best, bytes / best / 1e6,
+               best * 1e6 / rows);
+        fflush(stdout);
+    };
+    timeit("plain", [&] { hipLaunchKernelGGL(plain, dim3(P), dim3(256), 0, 0, (const float4*)X, rows, nv, out); });
+    timeit("plain1", [&] { hipLaunchKernelGGL(plain1, dim3(P), dim3(64), 0, 0, (const float4*)X, rows, nv, out); });
+    const int MB = (R + kMetaRows - 1) / kMetaRows + 2;
+    RingGeom g{R, MB, D, 0};
+    const size_t lds = sizeof(RingHeader) + (size_t)MB * kMetaBlockBytes + (size_t)R * rowbytes;
+    CK(hipFuncSetAttribute((const void*)ldsdma<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    timeit("ldsdma", [&] { hipLaunchKernelGGL(ldsdma<2>, dim3(P), dim3(128), lds, 0, L, g); });
+    int w = 0;
+    CK(hipMemcpy(&w, wd, 4, hipMemcpyDeviceToHost));
+    printf("watchdog=%d R=%d D=%d lds=%zu\n", w, R, D, lds);
+    return 0;
+}
