@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256) void chain_block(ChainLaunch L, KParams kp, Ri
     __syncthreads();
 
     if (wave == 1) {
-        ring_loader<S, NV, FULL>(L, dsc, hdr, meta_ring, ring, geom, lane);
+        ring_loader<S, NV, FULL, kBlk>(L, dsc, hdr, meta_ring, ring, geom, lane);
         return;
     }
 
@@ -472,21 +472,18 @@ static int launch_block(const ChainLaunch& L, const KParams& kp, bool full, size
     constexpr int ROW = NV * 1024;
     const size_t budget = lds > 0 ? lds : (size_t)64 * 1024;
     const size_t fixed = sizeof(RingHeader) + sizeof(GramHeader);
-    int D = 56 / NV;
-    if (D > 32) D = 32;
+    const int D = loader_depth<NV>();
     int R = 0, MB = 0, GS = 0;
     auto bytes_for = [&](int r) {
         const int mb = (r + kMetaRows - 1) / kMetaRows + 2;
         const int gs = r / kBlk + 1;
         return fixed + (size_t)mb * kMetaBlockBytes + (size_t)gs * kBlk * kBlk * 4 + (size_t)r * ROW;
     };
-    for (;;) {
-        R = (int)((budget - fixed) / ROW) / kBlk * kBlk;
-        while (R > 0 && bytes_for(R) > budget) R -= kBlk;
-        if (R >= D + kBlk || D == 1) break;
-        D = D > 2 ? D / 2 : 1;
-    }
-    if (R < D + kBlk) return (int)hipErrorInvalidValue;  // LDS budget too small for this d
+    // a block never wraps (R multiple of kBlk); one block beyond the loader's depth keeps the
+    // stream going while the chain wave holds a block
+    R = (int)((budget - fixed) / ROW) / kBlk * kBlk;
+    while (R > 0 && bytes_for(R) > budget) R -= kBlk;
+    if (R < 2 * kBlk) return (int)hipErrorInvalidValue;  // LDS budget too small for this d
     MB = (R + kMetaRows - 1) / kMetaRows + 2;
     GS = R / kBlk + 1;
     RingGeom g{R, MB, D, GS};

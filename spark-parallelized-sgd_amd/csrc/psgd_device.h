@@ -276,38 +276,69 @@ __device__ __forceinline__ void lds_store_u32_asm(unsigned* p, unsigned v) {
 // ------------------------------------------------------------------------------------------
 // The row loader wave (shared by chain_dense and chain_block): streams the partition's rows, in
 // iterator order, into an R-slot LDS ring with global_load_lds (LDS DMA, 1 KiB per instruction,
-// up to D rows in flight), plus each row's label and stepSize/sqrt(j) in 256-byte meta blocks
-// (one per 16 rows), and publishes hdr->ready = number of rows that have landed. It refills the
-// slot of row t only once hdr->consumed > t - R. Its own LDS accesses are inline asm so that
-// the compiler does not drain the DMA before them.
+// loader_depth(NV) rows in flight), plus each row's label and stepSize/sqrt(j) in 256-byte meta
+// blocks (one per 16 rows), and publishes hdr->ready = number of rows that have landed, every
+// PUB rows. It refills the slot of row t only once hdr->consumed > t - R; before it blocks on a
+// full ring it drains its DMA and publishes every row it has issued, so a consumer that waits
+// for any row inside the ring always makes progress. Its LDS accesses are inline asm so that
+// the compiler does not drain the DMA before them; the depth is a compile-time constant (a
+// runtime s_waitcnt needs a branch tree that costs more than the row).
 // ------------------------------------------------------------------------------------------
-template <typename S, int NV, bool FULL>
+template <int NV>
+__host__ __device__ constexpr int loader_depth() {
+    return NV == 1 ? 56 : NV == 2 ? 28 : NV == 4 ? 14 : 7;   // <= 56 instructions in vmcnt
+}
+
+__device__ __forceinline__ void lds_store_u32_nowait(unsigned* p, unsigned v) {
+    const unsigned addr = (unsigned)(uintptr_t)p;
+    asm volatile("ds_write_b32 %0, %1" : : "v"(addr), "v"(v) : "memory");
+}
+
+template <typename S, int NV, bool FULL, int PUB>
 __device__ __forceinline__ void ring_loader(const ChainLaunch& L, const ChainDesc& dsc, RingHeader* hdr,
                                             char* meta_ring, char* ring, const RingGeom& geom,
                                             int lane) {
     using V = typename Vec16<S>::type;
     constexpr int VEC = Vec16<S>::N;
     constexpr int ROW_BYTES = NV * 1024;
+    constexpr int D = loader_depth<NV>();
+    static_assert(kMetaRows % PUB == 0, "a meta block covers whole groups");
     const int64_t n = dsc.n_rows;
     const int R = geom.rows;
     const int MB = geom.meta_blocks;
-    const int D = geom.depth;
     const S* X = reinterpret_cast<const S*>(dsc.x);
     const int64_t ld = dsc.ld;
     // meta DMA lane l: row 16k + l/4, dword l%4 of {y lo, y hi, step lo, step hi}
     const unsigned* msrc = reinterpret_cast<const unsigned*>((lane & 2) ? L.steps : dsc.y) + (lane & 1);
     const int mrow = lane >> 2;
-    unsigned consumed = 0;
+    int64_t limit = R;            // rows < limit have a free slot
     int slot = 0, mslot = 0;
-    for (int64_t t = 0; t < n; ++t) {
-        if (t >= (int64_t)consumed + R) {
-            // ring full: wait for the consumer to free the slot of row t - R
-            // (R - D >= the consumer's block keeps enough rows published that this cannot deadlock)
+    auto issue_row = [&](int64_t t) __attribute__((always_inline)) {
+        char* dst = ring + slot * ROW_BYTES;
+        const V* row = reinterpret_cast<const V*>(X + t * ld);
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            if (FULL || (v * 64 + lane) * VEC < ld)
+                __builtin_amdgcn_global_load_lds(
+                    (const void*)(as_global(row + v * 64 + lane)),
+                    (__attribute__((address_space(3))) void*)(dst + v * 1024), 16, 0, 0);
+        }
+        slot = (slot + 1 == R) ? 0 : slot + 1;
+    };
+    // Rows go out in groups of PUB: one ring-space check, at most one meta DMA and one publish
+    // per group, no branch per row.
+    for (int64_t t = 0; t < n; t += PUB) {
+        const int64_t te = (t + PUB < n) ? t + PUB : n;
+        if (te > limit) {
+            // ring full: publish everything issued, then wait for the consumer to free slots
+            asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
+            lds_store_u32_nowait(&hdr->ready, (unsigned)t);
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             for (;;) {
-                consumed = lds_load_u32_asm(&hdr->consumed);
-                if (t < (int64_t)consumed + R) break;
-                if (lds_load_u32_asm(&hdr->stop)) goto drain;
+                const unsigned c = __builtin_amdgcn_readfirstlane(lds_load_u32_asm(&hdr->consumed));
+                limit = (int64_t)c + R;
+                if (te <= limit) break;
+                if (__builtin_amdgcn_readfirstlane(lds_load_u32_asm(&hdr->stop))) goto drain;
                 if (__builtin_amdgcn_s_memrealtime() - t0 > kWatchdogTicks) {
                     __hip_atomic_fetch_or(L.watchdog, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     lds_store_u32_asm(&hdr->stop, 1u);
@@ -322,29 +353,22 @@ __device__ __forceinline__ void ring_loader(const ChainLaunch& L, const ChainDes
             __builtin_amdgcn_global_load_lds(
                 (const void*)(as_global(msrc + 2 * r)),
                 (__attribute__((address_space(3))) void*)(meta_ring + mslot * kMetaBlockBytes), 4, 0, 0);
-            if (++mslot == MB) mslot = 0;
+            mslot = (mslot + 1 == MB) ? 0 : mslot + 1;
         }
-        {
-            char* dst = ring + slot * ROW_BYTES;
-            const V* row = reinterpret_cast<const V*>(X + t * ld);
+        if (te - t == PUB) {
 #pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                if (FULL || (v * 64 + lane) * VEC < ld)
-                    __builtin_amdgcn_global_load_lds(
-                        (const void*)(as_global(row + v * 64 + lane)),
-                        (__attribute__((address_space(3))) void*)(dst + v * 1024), 16, 0, 0);
-            }
+            for (int k = 0; k < PUB; ++k) issue_row(t + k);
+        } else {
+            for (int64_t u = t; u < te; ++u) issue_row(u);
         }
-        if (++slot == R) slot = 0;
-        if (t >= D) {
-            // all but the newest D rows' instructions are done: row t - D has landed
+        if (te > D) {
+            // all but the youngest D rows' instructions are done: rows < te - D have landed
             wait_vmcnt_le(D * NV);
-            lds_store_u32_asm(&hdr->ready, (unsigned)(t - D + 1));
+            lds_store_u32_nowait(&hdr->ready, (unsigned)(te - D));
         }
     }
 drain:
     asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
     lds_store_u32_asm(&hdr->ready, (unsigned)n);
 }
-
 }  // namespace psgd

@@ -54,7 +54,7 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, Ri
     __syncthreads();
 
     if (wave == 1) {
-        ring_loader<S, NV, FULL>(L, dsc, hdr, meta_ring, ring, geom, lane);
+        ring_loader<S, NV, FULL, 4>(L, dsc, hdr, meta_ring, ring, geom, lane);
         return;
     }
 
@@ -537,22 +537,18 @@ static int launch_reg(const ChainLaunch& L, const KParams& kp, bool full, size_t
     // (vmcnt holds at most 63 instructions, NV per row); R - D >= 8 slots stay published or
     // free so neither wave can wait on the other forever.
     constexpr int ROW = NV * 1024;
+    // Ring geometry from the per-workgroup LDS budget (`lds`: chosen by the host so that the
+    // chains spread evenly over the CUs); the consumer reads rows t and t+1, the loader keeps
+    // loader_depth rows in flight and drains before it blocks on a full ring.
     const size_t budget = lds > 0 ? lds : (size_t)64 * 1024;
-    int D = 56 / NV;
-    if (D > 32) D = 32;
-    int R = 0, MB = 0;
-    for (;;) {
-        // rows that fit: header + meta blocks + rows
-        R = (int)((budget - sizeof(RingHeader) - 3 * kMetaBlockBytes) / ROW);
+    const int D = loader_depth<NV>();
+    int R = (int)((budget - sizeof(RingHeader) - 3 * kMetaBlockBytes) / ROW);
+    int MB = (R + kMetaRows - 1) / kMetaRows + 2;
+    while (R > 0 && sizeof(RingHeader) + (size_t)MB * kMetaBlockBytes + (size_t)R * ROW > budget) {
+        --R;
         MB = (R + kMetaRows - 1) / kMetaRows + 2;
-        while (R > 0 && sizeof(RingHeader) + (size_t)MB * kMetaBlockBytes + (size_t)R * ROW > budget) {
-            --R;
-            MB = (R + kMetaRows - 1) / kMetaRows + 2;
-        }
-        if (R >= D + 8 || D == 1) break;
-        D = D > 2 ? D / 2 : 1;
     }
-    if (R < D + 3) return (int)hipErrorInvalidValue;  // LDS budget too small for this d
+    if (R < 6) return (int)hipErrorInvalidValue;  // LDS budget too small for this d (R >= PUB + 2)
     RingGeom g{R, MB, D, 0};
     const size_t bytes = sizeof(RingHeader) + (size_t)MB * kMetaBlockBytes + (size_t)R * ROW;
     if (full) {

@@ -47,6 +47,49 @@ __global__ __launch_bounds__(64) void plain1(const float4* __restrict__ X, int64
     if (acc.x == 1234.5f) out[0] = acc.y + acc.z + acc.w;
 }
 
+
+// NW waves per workgroup, each streaming a contiguous share of the partition with U 16-byte
+// loads per lane in flight (loads to registers).
+template <int NW, int U>
+__global__ __launch_bounds__(NW * 64) void regstream(const float4* __restrict__ X, int64_t rows_per,
+                                                     int nv, float* out) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t total = rows_per * nv;          // 1 KiB pieces in the partition
+    const int64_t a = total * wave / NW, b = total * (wave + 1) / NW;
+    const float4* base = X + (int64_t)blockIdx.x * total * 64;
+    float4 acc = {0, 0, 0, 0};
+    int64_t i = a;
+    for (; i + U <= b; i += U) {
+        float4 x[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) x[k] = base[(i + k) * 64 + lane];
+#pragma unroll
+        for (int k = 0; k < U; ++k) { acc.x += x[k].x; acc.y += x[k].y; acc.z += x[k].z; acc.w += x[k].w; }
+    }
+    for (; i < b; ++i) { float4 x = base[i * 64 + lane]; acc.x += x.x; }
+    if (acc.x == 1234.5f) out[0] = acc.y + acc.z + acc.w;
+}
+
+// NW loader waves per workgroup, each LDS-DMAing its contiguous share of the partition into its
+// own 32 KiB LDS region (overwritten, no consumer), keeping D pieces (1 KiB each) in flight.
+template <int NW, int D>
+__global__ __launch_bounds__(NW * 64) void dmaraw(const float4* __restrict__ X, int64_t rows_per, int nv) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t total = rows_per * nv;
+    const int64_t a = total * wave / NW, b = total * (wave + 1) / NW;
+    const float4* base = X + (int64_t)blockIdx.x * total * 64;
+    char* region = smem + wave * 32768;
+    int slot = 0;
+    for (int64_t i = a; i < b; ++i) {
+        __builtin_amdgcn_global_load_lds((const void*)(as_global(base + i * 64 + lane)),
+                                         (__attribute__((address_space(3))) void*)(region + slot * 1024), 16, 0, 0);
+        slot = (slot + 1) & 31;
+        wait_vmcnt_le(D);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 template <int NV>
 __global__ __launch_bounds__(128) void ldsdma(ChainLaunch L, RingGeom geom) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -58,7 +101,7 @@ __global__ __launch_bounds__(128) void ldsdma(ChainLaunch L, RingGeom geom) {
     if (threadIdx.x == 0) { hdr->ready = 0; hdr->consumed = 0; hdr->stop = 0; }
     __syncthreads();
     if (wave == 1) {
-        ring_loader<float, NV, true>(L, dsc, hdr, meta_ring, ring, geom, lane);
+        ring_loader<float, NV, true, 8>(L, dsc, hdr, meta_ring, ring, geom, lane);
         return;
     }
     const int64_t n = dsc.n_rows;
@@ -67,6 +110,78 @@ __global__ __launch_bounds__(128) void ldsdma(ChainLaunch L, RingGeom geom) {
         ready = __hip_atomic_load(&hdr->ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_store(&hdr->consumed, ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+
+// ring_loader variants: PUB = rows per `ready` publish (0: only at the end), DC = compile-time
+// depth (0: runtime switch), META = meta DMA on/off, CONS = consult `consumed` (ring flow control).
+template <int PUB, int DC, bool META, bool CONS>
+__device__ void loader_var(const ChainLaunch& L, const ChainDesc& dsc, RingHeader* hdr, char* meta_ring,
+                           char* ring, const RingGeom& geom, int lane) {
+    constexpr int NV = 2;
+    using V = f32x4;
+    constexpr int ROW_BYTES = NV * 1024;
+    const int64_t n = dsc.n_rows;
+    const int R = geom.rows, MB = geom.meta_blocks;
+    const int D = DC ? DC : geom.depth;
+    const float* X = reinterpret_cast<const float*>(dsc.x);
+    const int64_t ld = dsc.ld;
+    const unsigned* msrc = reinterpret_cast<const unsigned*>((lane & 2) ? L.steps : dsc.y) + (lane & 1);
+    const int mrow = lane >> 2;
+    unsigned consumed = 0;
+    int slot = 0, mslot = 0;
+    for (int64_t t = 0; t < n; ++t) {
+        if (CONS && t >= (int64_t)consumed + R) {
+            for (;;) {
+                consumed = lds_load_u32_asm(&hdr->consumed);
+                if (t < (int64_t)consumed + R) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        if (META && (t & (kMetaRows - 1)) == 0) {
+            int64_t r = t + mrow;
+            if (r >= n) r = n - 1;
+            __builtin_amdgcn_global_load_lds((const void*)(as_global(msrc + 2 * r)),
+                (__attribute__((address_space(3))) void*)(meta_ring + mslot * kMetaBlockBytes), 4, 0, 0);
+            if (++mslot == MB) mslot = 0;
+        }
+        char* dst = ring + slot * ROW_BYTES;
+        const V* row = reinterpret_cast<const V*>(X + t * ld);
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+            __builtin_amdgcn_global_load_lds((const void*)(as_global(row + v * 64 + lane)),
+                                             (__attribute__((address_space(3))) void*)(dst + v * 1024), 16, 0, 0);
+        if (++slot == R) slot = 0;
+        if (t >= D) {
+            if (DC) wait_vmcnt_le(DC * NV); else wait_vmcnt_le(D * NV);
+            if (PUB && ((t + 1) % PUB) == 0) lds_store_u32_asm(&hdr->ready, (unsigned)(t - D + 1));
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
+    lds_store_u32_asm(&hdr->ready, (unsigned)n);
+}
+
+template <int PUB, int DC, bool META, bool CONS>
+__global__ __launch_bounds__(128) void ldsvar(ChainLaunch L, RingGeom geom) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    RingHeader* hdr = reinterpret_cast<RingHeader*>(smem);
+    char* meta_ring = smem + sizeof(RingHeader);
+    char* ring = meta_ring + geom.meta_blocks * kMetaBlockBytes;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const ChainDesc dsc = L.descs[blockIdx.x];
+    if (threadIdx.x == 0) { hdr->ready = 0; hdr->consumed = 0; hdr->stop = 0; }
+    __syncthreads();
+    if (wave == 1) {
+        loader_var<PUB, DC, META, CONS>(L, dsc, hdr, meta_ring, ring, geom, lane);
+        return;
+    }
+    const int64_t n = dsc.n_rows;
+    unsigned ready = 0;
+    while ((int64_t)ready < n) {
+        ready = __hip_atomic_load(&hdr->ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(&hdr->consumed, ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __builtin_amdgcn_s_sleep(8);
     }
 }
 
@@ -118,11 +233,20 @@ int main(int argc, char** argv) {
     };
     timeit("plain", [&] { hipLaunchKernelGGL(plain, dim3(P), dim3(256), 0, 0, (const float4*)X, rows, nv, out); });
     timeit("plain1", [&] { hipLaunchKernelGGL(plain1, dim3(P), dim3(64), 0, 0, (const float4*)X, rows, nv, out); });
+#define RS(NW, U) timeit("reg" #NW "x" #U, [&] { hipLaunchKernelGGL((regstream<NW, U>), dim3(P), dim3(NW * 64), 0, 0, (const float4*)X, rows, nv, out); });
+    RS(1, 32) RS(2, 16) RS(4, 8) RS(4, 16) RS(8, 8) RS(8, 16) RS(16, 4) RS(16, 8)
+#define DR(NW, D) CK(hipFuncSetAttribute((const void*)dmaraw<NW, D>, hipFuncAttributeMaxDynamicSharedMemorySize, NW * 32768)); \
+    timeit("dma" #NW "x" #D, [&] { hipLaunchKernelGGL((dmaraw<NW, D>), dim3(P), dim3(NW * 64), NW * 32768, 0, (const float4*)X, rows, nv); });
+    DR(1, 16) DR(1, 32) DR(1, 56) DR(2, 16) DR(2, 28) DR(4, 8) DR(4, 14)
     const int MB = (R + kMetaRows - 1) / kMetaRows + 2;
     RingGeom g{R, MB, D, 0};
     const size_t lds = sizeof(RingHeader) + (size_t)MB * kMetaBlockBytes + (size_t)R * rowbytes;
     CK(hipFuncSetAttribute((const void*)ldsdma<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     timeit("ldsdma", [&] { hipLaunchKernelGGL(ldsdma<2>, dim3(P), dim3(128), lds, 0, L, g); });
+#define LV(PUB, DC, META, CONS) CK(hipFuncSetAttribute((const void*)ldsvar<PUB, DC, META, CONS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+    timeit("v" #PUB "_" #DC "_" #META "_" #CONS, [&] { hipLaunchKernelGGL((ldsvar<PUB, DC, META, CONS>), dim3(P), dim3(128), lds, 0, L, g); });
+    LV(1, 0, true, true) LV(1, 28, true, true) LV(8, 28, true, true) LV(0, 28, true, false)
+    LV(0, 28, false, false) LV(8, 28, false, true) LV(1, 28, false, false) LV(8, 28, true, false)
     int w = 0;
     CK(hipMemcpy(&w, wd, 4, hipMemcpyDeviceToHost));
     printf("watchdog=%d R=%d D=%d lds=%zu\n", w, R, D, lds);
