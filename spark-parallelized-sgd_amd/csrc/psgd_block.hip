@@ -36,6 +36,7 @@ namespace psgd {
 
 constexpr int kBlk = 8;           // rows per block
 constexpr int kPairs = 28;        // kBlk*(kBlk-1)/2 Gram entries below the diagonal
+static_assert(kMetaRows == 2 * kBlk, "a meta block holds two row blocks");
 
 struct GramHeader {
     unsigned gdone[2];   // blocks finished by Gram wave 0 (even blocks) / 1 (odd blocks)
@@ -130,7 +131,7 @@ __device__ __forceinline__ float row_loss(float z, float y, float aux) {
 }
 
 template <typename S, int GRAD, int UPD, int NV, bool FULL>
-__global__ __launch_bounds__(256) void chain_block(ChainLaunch L, KParams kp, RingGeom geom) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void chain_block(ChainLaunch L, KParams kp, RingGeom geom) {
     using V = typename Vec16<S>::type;
     using T2 = float __attribute__((ext_vector_type(2)));
     constexpr int VEC = Vec16<S>::N;
@@ -138,7 +139,7 @@ __global__ __launch_bounds__(256) void chain_block(ChainLaunch L, KParams kp, Ri
     constexpr int E2 = E / 2;
     constexpr int H = VEC / 2;             // pairs per 16-byte vector
     constexpr int ROW_BYTES = NV * 1024;
-    constexpr bool KEEP = E2 * kBlk <= 64; // the chain wave keeps a block's rows in registers
+    constexpr bool KEEP = E2 * kBlk <= 32; // the chain wave keeps two blocks of rows in registers
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // LDS: [RingHeader 16 B][GramHeader 16 B][meta ring MB x 256 B][Gram ring GS x 256 B]
     //      [row ring R x ROW_BYTES]
@@ -222,11 +223,18 @@ __global__ __launch_bounds__(256) void chain_block(ChainLaunch L, KParams kp, Ri
         }
         unsigned ready = 0;
         unsigned done = 0;
+        int rs = gw * kBlk;          // ring slot of the block's first row (R is a multiple of 16)
+        int gs = gw;                 // Gram slot of the block
+        PSGD_STAMP(const uint64_t st_begin = __builtin_amdgcn_s_memtime(); uint64_t st_rd = 0;)
         for (int64_t b = gw; b < nblk; b += 2) {
             const int64_t t0 = b * kBlk;
             const int64_t kk = (n - t0) < kBlk ? (n - t0) : kBlk;
+            PSGD_STAMP(const uint64_t st_w = __builtin_amdgcn_s_memtime();)
             if (!wait_ready(ready, t0 + kk, 4)) break;
-            const char* base = ring + (int)(t0 % R) * ROW_BYTES;
+            PSGD_STAMP(st_rd += __builtin_amdgcn_s_memtime() - st_w;)
+            const char* base = ring + rs * ROW_BYTES;
+            rs += 2 * kBlk;
+            if (rs >= R) rs -= R;
             T2 acc[kPairs];
 #pragma unroll
             for (int q = 0; q < kPairs; ++q) acc[q] = T2{0.0f, 0.0f};
@@ -250,11 +258,17 @@ __global__ __launch_bounds__(256) void chain_block(ChainLaunch L, KParams kp, Ri
 #pragma unroll
             for (int q = kPairs; q < 32; ++q) g[q] = 0.0f;
             const float val = reduce32(g, lane);
-            float* slot = gring + (int)(b % GS) * (kBlk * kBlk);
+            float* slot = gring + gs * (kBlk * kBlk);
+            gs += 2;
+            if (gs >= GS) gs -= GS;
             if (goff >= 0) slot[goff] = val;
             ++done;
             __hip_atomic_store(&ghdr->gdone[gw], done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
+        PSGD_STAMP(if (L.stamps && lane == 0) {
+            unsigned long long* o = L.stamps + (size_t)chain * 16 + 8 + 4 * gw;
+            o[0] = __builtin_amdgcn_s_memtime() - st_begin; o[1] = st_rd;
+        })
         return;
     }
 
@@ -277,38 +291,91 @@ __global__ __launch_bounds__(256) void chain_block(ChainLaunch L, KParams kp, Ri
     float loss_blk = 0.0f;
     int64_t count = 0;
     unsigned ready = 0;
+    int rs = 0, gs = 0, ms = 0;      // ring slot, Gram slot and meta block of the current block
+    const int64_t nfull = n / kBlk;
+    const int ntail = (int)(n - nfull * kBlk);
+    PSGD_STAMP(const uint64_t st_begin = __builtin_amdgcn_s_memtime(); uint64_t st_rd = 0, st_gr = 0, st_p = 0, st_rec = 0, st_upd = 0;)
 
-    for (int64_t b = 0; b < nblk; ++b) {
-        const int64_t t0 = b * kBlk;
-        const int kk = (n - t0) < kBlk ? (int)(n - t0) : kBlk;
-        if (!wait_ready(ready, t0 + kk, 2)) break;
-        const char* base = ring + (int)(t0 % R) * ROW_BYTES;
-
-        // p_k = x_k . W (stale rows k >= kk give garbage in lanes that are never read)
-        T2 xk[KEEP ? kBlk : 1][KEEP ? E2 : 1];
-        float pk[kBlk];
+    auto wait_rows = [&](int64_t rows) __attribute__((always_inline)) -> bool {
+        PSGD_STAMP(const uint64_t st_w = __builtin_amdgcn_s_memtime();)
+        const bool ok = wait_ready(ready, rows, 2);
+        PSGD_STAMP(st_rd += __builtin_amdgcn_s_memtime() - st_w;)
+        return ok;
+    };
+    // A block's rows from the ring into registers; rows >= kk (a tail block) read as zero.
+    auto load_rows = [&](auto tail_c, T2 (&xr)[kBlk][E2], const char* base, int kk) __attribute__((always_inline)) {
+        constexpr bool TAIL = decltype(tail_c)::value;
 #pragma unroll
         for (int k = 0; k < kBlk; ++k) {
-            T2 a0 = T2{0.0f, 0.0f}, a1 = T2{0.0f, 0.0f};
 #pragma unroll
             for (int v = 0; v < NV; ++v) {
                 T2 xv[H];
                 to_pairs(read_vec(base + k * ROW_BYTES, v), xv);
 #pragma unroll
-                for (int h = 0; h < H; ++h) {
-                    const int e = v * H + h;
-                    if (e & 1) a1 = __builtin_elementwise_fma(xv[h], w[e], a1);
-                    else a0 = __builtin_elementwise_fma(xv[h], w[e], a0);
-                    if constexpr (KEEP) xk[k][e] = xv[h];
+                for (int h = 0; h < H; ++h) xr[k][v * H + h] = (TAIL && k >= kk) ? T2{0.0f, 0.0f} : xv[h];
+            }
+        }
+    };
+
+    // One block: rows in xr (KEEP) or in the ring at `base`; kk rows (kBlk unless TAIL).
+    auto block = [&](auto tail_c, T2 (&xr)[kBlk][E2], int64_t b, int kk, const char* base)
+                     __attribute__((always_inline)) -> bool {
+        constexpr bool TAIL = decltype(tail_c)::value;
+        const int64_t t0 = b * kBlk;
+        // this lane's row: label and step
+        const f64x2 meta = *reinterpret_cast<const f64x2*>(
+            meta_ring + ms * kMetaBlockBytes + ((int)(b & 1) * kBlk + krow) * 16);
+        // the block's Gram triangle (Gram wave b&1 publishes blocks in order)
+        PSGD_STAMP(const uint64_t st_g = __builtin_amdgcn_s_memtime();)
+        {
+            const unsigned need = (unsigned)(b >> 1) + 1;
+            unsigned* gd = &ghdr->gdone[b & 1];
+            if (__hip_atomic_load(gd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+                const uint64_t tw = __builtin_amdgcn_s_memrealtime();
+                while (__hip_atomic_load(gd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+                    if (__builtin_amdgcn_s_memrealtime() - tw > kWatchdogTicks) {
+                        __hip_atomic_fetch_or(L.watchdog, 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        return false;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
                 }
             }
-            const T2 a = a0 + a1;
+        }
+        PSGD_STAMP(st_gr += __builtin_amdgcn_s_memtime() - st_g;)
+        const float* grow = gring + gs * (kBlk * kBlk) + krow * kBlk;
+        const f32x4 g0 = *reinterpret_cast<const f32x4*>(grow);
+        const f32x4 g1 = *reinterpret_cast<const f32x4*>(grow + 4);
+        const float G[kBlk] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+        if constexpr (KEEP) {
+            // the block's rows are in registers (G and meta slots live until the next block's
+            // rows are handed back): free its ring slots
+            __hip_atomic_store(&hdr->consumed, (unsigned)(t0 + kk), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+
+        // p_k = x_k . W (one packed accumulator per row; eight rows interleave)
+        PSGD_STAMP(const uint64_t st_a = __builtin_amdgcn_s_memtime();)
+        float pk[kBlk];
+#pragma unroll
+        for (int k = 0; k < kBlk; ++k) {
+            T2 a;
+            if constexpr (KEEP) {
+                a = xr[k][0] * w[0];
+#pragma unroll
+                for (int e = 1; e < E2; ++e) a = __builtin_elementwise_fma(xr[k][e], w[e], a);
+            } else {
+                a = T2{0.0f, 0.0f};
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    T2 xv[H];
+                    to_pairs(read_vec(base + k * ROW_BYTES, v), xv);
+#pragma unroll
+                    for (int h = 0; h < H; ++h) a = __builtin_elementwise_fma(xv[h], w[v * H + h], a);
+                }
+            }
             pk[k] = a.x + a.y;
         }
-        // this lane's row: label and step
-        const int64_t tr = t0 + krow;
-        const f64x2 meta = *reinterpret_cast<const f64x2*>(
-            meta_ring + (int)((tr / kMetaRows) % MB) * kMetaBlockBytes + (int)(tr % kMetaRows) * 16);
         const float yv = float(meta.x), sv = float(meta.y);
         const float nsv = -sv;
         float aux;
@@ -317,74 +384,30 @@ __global__ __launch_bounds__(256) void chain_block(ChainLaunch L, KParams kp, Ri
         else aux = 0.0f;
         const float alpha = 1.0f - sv * lam;      // SquaredL2 shrink of this lane's row
         float z = reduce8(pk, lane);
-
-        // the block's Gram triangle (Gram wave b&1 publishes blocks in order)
-        {
-            const unsigned need = (unsigned)(b >> 1) + 1;
-            unsigned* gd = &ghdr->gdone[b & 1];
-            if (__hip_atomic_load(gd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
-                const uint64_t tw = __builtin_amdgcn_s_memrealtime();
-                bool ok = true;
-                while (__hip_atomic_load(gd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
-                    if (__builtin_amdgcn_s_memrealtime() - tw > kWatchdogTicks) {
-                        __hip_atomic_fetch_or(L.watchdog, 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        ok = false;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                if (!ok) break;
-            }
-        }
-        const float* grow = gring + (int)(b % GS) * (kBlk * kBlk) + krow * kBlk;
-        const f32x4 g0 = *reinterpret_cast<const f32x4*>(grow);
-        const f32x4 g1 = *reinterpret_cast<const f32x4*>(grow + 4);
-        const float G[kBlk] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
-        if constexpr (KEEP) {
-            // rows, labels, steps and the Gram row are in registers: free the slots
-            __hip_atomic_store(&hdr->consumed, (unsigned)(t0 + kk), __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
+        PSGD_STAMP(const uint64_t st_b = __builtin_amdgcn_s_memtime(); st_p += st_b - st_a;)
 
         // the scalar recurrence: c_i from z_i, then every later row's dot moves by c_i G[k][i]
         // (SquaredL2 also shrinks the finished rows' z: zf keeps z_k for the loss)
         float c[kBlk], al[kBlk];
         float zf = z;
-        if (kk == kBlk) {
 #pragma unroll
-            for (int i = 0; i < kBlk; ++i) {
-                c[i] = readlane_f(coef<GRAD>(z, yv, sv, nsv, aux), row_lane(i));
-                if constexpr (UPD == U_SQUARED_L2) {
-                    if (krow == i) zf = z;
-                    al[i] = readlane_f(alpha, row_lane(i));
-                    if (i + 1 < kBlk) z = __builtin_fmaf(c[i], G[i], al[i] * z);
-                } else {
-                    if (i + 1 < kBlk) z = __builtin_fmaf(c[i], G[i], z);
-                }
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < kBlk; ++i) {
-                c[i] = 0.0f;
-                al[i] = 1.0f;
-                if (i < kk) {
-                    c[i] = readlane_f(coef<GRAD>(z, yv, sv, nsv, aux), row_lane(i));
-                    if constexpr (UPD == U_SQUARED_L2) {
-                        if (krow == i) zf = z;
-                        al[i] = readlane_f(alpha, row_lane(i));
-                        z = __builtin_fmaf(c[i], G[i], al[i] * z);
-                    } else {
-                        z = __builtin_fmaf(c[i], G[i], z);
-                    }
-                }
+        for (int i = 0; i < kBlk; ++i) {
+            c[i] = readlane_f(coef<GRAD>(z, yv, sv, nsv, aux), row_lane(i));
+            if constexpr (TAIL) c[i] = i < kk ? c[i] : 0.0f;
+            if constexpr (UPD == U_SQUARED_L2) {
+                if (krow == i) zf = z;
+                al[i] = readlane_f(alpha, row_lane(i));
+                if constexpr (TAIL) al[i] = i < kk ? al[i] : 1.0f;
+                if (i + 1 < kBlk) z = __builtin_fmaf(c[i], G[i], al[i] * z);
+            } else {
+                if (i + 1 < kBlk) z = __builtin_fmaf(c[i], G[i], z);
             }
         }
-        // z (zf for SquaredL2) now holds z_k in every lane of row k
         if constexpr (UPD != U_SQUARED_L2) zf = z;
+        PSGD_STAMP(const uint64_t st_c = __builtin_amdgcn_s_memtime(); st_rec += st_c - st_b;)
         {
             const float l = row_loss<GRAD>(zf, yv, aux);
-            if (loss_lane && krow < kk) loss_blk += l;
+            if (loss_lane && (!TAIL || krow < kk)) loss_blk += l;
             if ((b & 3) == 3) { loss_sum += double(loss_blk); loss_blk = 0.0f; }
         }
         count += kk;
@@ -392,40 +415,66 @@ __global__ __launch_bounds__(256) void chain_block(ChainLaunch L, KParams kp, Ri
         // W <- a_i W + c_i x_i, i = 0..kk-1, in sample order
 #pragma unroll
         for (int i = 0; i < kBlk; ++i) {
-            if (kk == kBlk || i < kk) {
-                const T2 ci = T2{c[i], c[i]};
-                if constexpr (KEEP) {
+            const T2 ci = T2{c[i], c[i]};
+            if constexpr (KEEP) {
 #pragma unroll
-                    for (int e = 0; e < E2; ++e) {
+                for (int e = 0; e < E2; ++e) {
+                    if constexpr (UPD == U_SQUARED_L2)
+                        w[e] = __builtin_elementwise_fma(ci, xr[i][e], w[e] * T2{al[i], al[i]});
+                    else
+                        w[e] = __builtin_elementwise_fma(ci, xr[i][e], w[e]);
+                }
+            } else if (!TAIL || i < kk) {
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    T2 xv[H];
+                    to_pairs(read_vec(base + i * ROW_BYTES, v), xv);
+#pragma unroll
+                    for (int h = 0; h < H; ++h) {
+                        const int e = v * H + h;
                         if constexpr (UPD == U_SQUARED_L2)
-                            w[e] = __builtin_elementwise_fma(ci, xk[i][e], w[e] * T2{al[i], al[i]});
+                            w[e] = __builtin_elementwise_fma(ci, xv[h], w[e] * T2{al[i], al[i]});
                         else
-                            w[e] = __builtin_elementwise_fma(ci, xk[i][e], w[e]);
-                    }
-                } else {
-#pragma unroll
-                    for (int v = 0; v < NV; ++v) {
-                        T2 xv[H];
-                        to_pairs(read_vec(base + i * ROW_BYTES, v), xv);
-#pragma unroll
-                        for (int h = 0; h < H; ++h) {
-                            const int e = v * H + h;
-                            if constexpr (UPD == U_SQUARED_L2)
-                                w[e] = __builtin_elementwise_fma(ci, xv[h], w[e] * T2{al[i], al[i]});
-                            else
-                                w[e] = __builtin_elementwise_fma(ci, xv[h], w[e]);
-                        }
+                            w[e] = __builtin_elementwise_fma(ci, xv[h], w[e]);
                     }
                 }
             }
         }
         if constexpr (!KEEP) {
-            __hip_atomic_store(&hdr->consumed, (unsigned)(t0 + kk), __ATOMIC_RELEASE,
+            __hip_atomic_store(&hdr->consumed, (unsigned)(t0 + kk), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
         }
+        PSGD_STAMP(st_upd += __builtin_amdgcn_s_memtime() - st_c;)
+        rs += kBlk;
+        if (rs == R) rs = 0;
+        if (++gs == GS) gs = 0;
+        if ((b & 1) && ++ms == MB) ms = 0;
+        return true;
+    };
+
+    using Full = std::integral_constant<bool, false>;
+    using Tail = std::integral_constant<bool, true>;
+    T2 xr[kBlk][E2];
+    bool ok = true;
+    for (int64_t b = 0; ok && b < nfull; ++b) {
+        ok = wait_rows((b + 1) * kBlk);
+        if (!ok) break;
+        const char* base = ring + rs * ROW_BYTES;
+        if constexpr (KEEP) load_rows(Full{}, xr, base, kBlk);
+        ok = block(Full{}, xr, b, kBlk, base);
+    }
+    if (ok && ntail > 0 && wait_rows(n)) {
+        const char* base = ring + rs * ROW_BYTES;
+        if constexpr (KEEP) load_rows(Tail{}, xr, base, ntail);
+        block(Tail{}, xr, nfull, ntail, base);
     }
     // a wave that stopped early leaves the others blocked on it: wake them
     __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    PSGD_STAMP(if (L.stamps && lane == 0) {
+        unsigned long long* o = L.stamps + (size_t)chain * 16;
+        o[0] = __builtin_amdgcn_s_memtime() - st_begin; o[1] = st_rd; o[2] = st_gr;
+        o[3] = st_p; o[12 + 2] = st_rec; o[12 + 3] = st_upd;
+    })
     loss_sum += double(loss_blk);
     // the loss partials of the 8 loss lanes
     {

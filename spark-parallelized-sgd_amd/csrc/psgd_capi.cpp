@@ -471,6 +471,7 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
     L.cnt = ctx->cnt.as<int64_t>();
     L.steps = ctx->steps.as<double>();
     L.watchdog = ctx->watchdog.as<int>();
+    L.stamps = nullptr;
     HIP_TRY(hipMemsetAsync(L.watchdog, 0, 16, st));
     psgd::KParams kp;
     kp.reg = params->reg_param;

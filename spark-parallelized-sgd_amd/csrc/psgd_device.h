@@ -316,23 +316,31 @@ __device__ __forceinline__ void ring_loader(const ChainLaunch& L, const ChainDes
     auto issue_row = [&](int64_t t) __attribute__((always_inline)) {
         char* dst = ring + slot * ROW_BYTES;
         const V* row = reinterpret_cast<const V*>(X + t * ld);
+        // every lane issues (past the row end it re-reads the row's first vector, bytes the
+        // consumers ignore): each row is exactly NV vmcnt entries, which the counted waits need
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
-            if (FULL || (v * 64 + lane) * VEC < ld)
-                __builtin_amdgcn_global_load_lds(
-                    (const void*)(as_global(row + v * 64 + lane)),
-                    (__attribute__((address_space(3))) void*)(dst + v * 1024), 16, 0, 0);
+            const V* src = (FULL || (v * 64 + lane) * VEC < ld) ? row + v * 64 + lane : row;
+            __builtin_amdgcn_global_load_lds(
+                (const void*)(as_global(src)),
+                (__attribute__((address_space(3))) void*)(dst + v * 1024), 16, 0, 0);
         }
         slot = (slot + 1 == R) ? 0 : slot + 1;
     };
     // Rows go out in groups of PUB: one ring-space check, at most one meta DMA and one publish
     // per group, no branch per row.
+    PSGD_STAMP(const uint64_t st_begin = __builtin_amdgcn_s_memtime(); uint64_t st_full = 0, st_vm = 0;)
     for (int64_t t = 0; t < n; t += PUB) {
         const int64_t te = (t + PUB < n) ? t + PUB : n;
         if (te > limit) {
-            // ring full: publish everything issued, then wait for the consumer to free slots
-            asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
-            lds_store_u32_nowait(&hdr->ready, (unsigned)t);
+            PSGD_STAMP(const uint64_t st_w = __builtin_amdgcn_s_memtime();)
+            // ring full: wait for the consumer to free slots. A ring deeper than the loader's
+            // depth plus two groups always leaves the consumer published rows to work on; a
+            // shallower one publishes everything issued first (drains the DMA).
+            if (R < D + 2 * PUB) {
+                asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
+                lds_store_u32_nowait(&hdr->ready, (unsigned)t);
+            }
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             for (;;) {
                 const unsigned c = __builtin_amdgcn_readfirstlane(lds_load_u32_asm(&hdr->consumed));
@@ -346,6 +354,7 @@ __device__ __forceinline__ void ring_loader(const ChainLaunch& L, const ChainDes
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
+            PSGD_STAMP(st_full += __builtin_amdgcn_s_memtime() - st_w;)
         }
         if ((t & (kMetaRows - 1)) == 0) {
             int64_t r = t + mrow;
@@ -363,12 +372,18 @@ __device__ __forceinline__ void ring_loader(const ChainLaunch& L, const ChainDes
         }
         if (te > D) {
             // all but the youngest D rows' instructions are done: rows < te - D have landed
+            PSGD_STAMP(const uint64_t st_v = __builtin_amdgcn_s_memtime();)
             wait_vmcnt_le(D * NV);
+            PSGD_STAMP(st_vm += __builtin_amdgcn_s_memtime() - st_v;)
             lds_store_u32_nowait(&hdr->ready, (unsigned)(te - D));
         }
     }
 drain:
     asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
     lds_store_u32_asm(&hdr->ready, (unsigned)n);
+    PSGD_STAMP(if (L.stamps && lane == 0) {
+        unsigned long long* o = L.stamps + (size_t)blockIdx.x * 16 + 4;
+        o[0] = __builtin_amdgcn_s_memtime() - st_begin; o[1] = st_full; o[2] = st_vm;
+    })
 }
 }  // namespace psgd

@@ -40,7 +40,15 @@ struct ChainLaunch {
     int64_t* cnt;            // [n_chains]  count
     const double* steps;     // [n_max] stepSize / sqrt(j), j = 1..n_max
     int* watchdog;           // set by a wave whose partner stopped making progress
+    unsigned long long* stamps;  // per-wave cycle counters, diagnostic builds only (PSGD_STAMPS)
 };
+
+// Diagnostic builds (-DPSGD_STAMPS, tools/chain_bench.hip) count s_memtime cycles per wave.
+#ifdef PSGD_STAMPS
+#define PSGD_STAMP(...) __VA_ARGS__
+#else
+#define PSGD_STAMP(...)
+#endif
 
 // Host-side launchers implemented in psgd_kernels.hip. Return hipError_t as int.
 // storage: 0 = f64, 1 = f32; compute: 0 = f64, 1 = f32.

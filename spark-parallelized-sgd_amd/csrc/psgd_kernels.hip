@@ -79,6 +79,7 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, Ri
     // sample t computes.
     T2 xb[2][E2];
     double yb[2], sb[2];
+    int meta_blk = 0;
     auto read_row = [&](auto pc, const char* src, int64_t t) __attribute__((always_inline)) {
         constexpr int p = decltype(pc)::value;
 #pragma unroll
@@ -93,8 +94,10 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, Ri
 #pragma unroll
             for (int k = 0; k < VEC; k += 2) xb[p][(v * VEC + k) / 2] = T2{tmp[k], tmp[k + 1]};
         }
+        // rows are read in order: the meta block advances every kMetaRows rows
+        if (t > 0 && (t & (kMetaRows - 1)) == 0) meta_blk = (meta_blk + 1 == MB) ? 0 : meta_blk + 1;
         const f64x2 meta = *reinterpret_cast<const f64x2*>(
-            meta_ring + ((t / kMetaRows) % MB) * kMetaBlockBytes + (t % kMetaRows) * 16);
+            meta_ring + meta_blk * kMetaBlockBytes + (int)(t & (kMetaRows - 1)) * 16);
         yb[p] = meta.x;
         sb[p] = meta.y;
     };
