@@ -31,6 +31,24 @@ WORKLOADS = {
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
+def pmc_traffic(workload, grad, variant, storage):
+    """HBM bytes per chain-kernel launch from the newest committed rocprofv3 PMC summary of the
+    same workload and kernel instance (profiles/r*_<workload>_pmc.json, tools/profile_round.sh +
+    tools/pmc_summary.py; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_pmc.json")))
+    if not files or not (300 <= variant < 400):
+        return None, None
+    g = {"logistic": 0, "least_squares": 1, "hinge": 2}[grad]
+    prefix = f"psgd::chain_block<{'float' if storage == 'f32' else 'double'}, {g}, 0, {variant - 300},"
+    with open(files[-1]) as f:
+        summ = json.load(f)
+    for name, e in summ.get("kernels", {}).items():
+        if name.startswith(prefix) and "hbm_bytes" in e:
+            return e["hbm_bytes"], os.path.relpath(files[-1], ROOT)
+    return None, None
+
+
 def kernel_name(variant):
     if 300 <= variant < 400:
         return f"chain_block (NV={variant - 300}: blocked fp32 chain, 8-row Gram blocks)"
@@ -202,6 +220,7 @@ def main():
     local_samples = n
     # one chain-kernel launch processes every row of this GPU's partitions
     achieved = local_samples * bytes_per_sample / avg_kernel_s / 1e9
+    traffic, traffic_src = pmc_traffic(args.workload, grad, engine.ctx.last_kernel(), sdt)
     out = {
         "metric": "training samples/sec (whole node) + achieved HBM GB/s, logistic SGD 1/2/4/8 GPUs",
         "value": value, "unit": "samples/s", "n_gpus": world, "steps": args.steps,
@@ -213,7 +232,8 @@ def main():
                    "step_size": step, "convergence_tol": 0.0, "mini_batch_fraction": 1.0,
                    "parallelism": f"dp{world} (chains sharded, RCCL all-gather + fold per epoch)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "kernel": kernel_name(engine.ctx.last_kernel()),
                      "bytes_per_launch": local_samples * bytes_per_sample,
                      "bytes_per_sample": bytes_per_sample, "avg_kernel_ms": avg_kernel_s * 1e3,

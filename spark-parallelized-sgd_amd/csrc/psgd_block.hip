@@ -115,6 +115,13 @@ __device__ __forceinline__ float coef(float z, float y, float s, float ns, float
     }
 }
 
+// MLUtils.log1pExp with the hardware exp2/log2 (fp32 throughput mode: ~1e-7 absolute)
+__device__ __forceinline__ float fast_log1p_exp(float x) {
+    const float ax = __builtin_fabsf(x);
+    const float l = __logf(1.0f + __expf(-ax));
+    return x > 0.0f ? x + l : l;
+}
+
 template <int GRAD>
 __device__ __forceinline__ float row_loss(float z, float y, float aux) {
     if constexpr (GRAD == G_LEAST_SQUARES) {
@@ -122,7 +129,7 @@ __device__ __forceinline__ float row_loss(float z, float y, float aux) {
         return m * m;                                  // halved once at the end (exact)
     } else if constexpr (GRAD == G_LOGISTIC) {
         const float margin = -z;
-        const float l = log1p_exp(margin);
+        const float l = fast_log1p_exp(margin);
         return y > 0.0f ? l : l - margin;
     } else {
         const float lz = aux * z;
@@ -139,7 +146,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     constexpr int E2 = E / 2;
     constexpr int H = VEC / 2;             // pairs per 16-byte vector
     constexpr int ROW_BYTES = NV * 1024;
-    constexpr bool KEEP = E2 * kBlk <= 32; // the chain wave keeps two blocks of rows in registers
+    constexpr bool KEEP = E2 * kBlk <= 64; // the chain wave keeps a block's rows in registers
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // LDS: [RingHeader 16 B][GramHeader 16 B][meta ring MB x 256 B][Gram ring GS x 256 B]
     //      [row ring R x ROW_BYTES]
@@ -325,35 +332,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         // this lane's row: label and step
         const f64x2 meta = *reinterpret_cast<const f64x2*>(
             meta_ring + ms * kMetaBlockBytes + ((int)(b & 1) * kBlk + krow) * 16);
-        // the block's Gram triangle (Gram wave b&1 publishes blocks in order)
-        PSGD_STAMP(const uint64_t st_g = __builtin_amdgcn_s_memtime();)
-        {
-            const unsigned need = (unsigned)(b >> 1) + 1;
-            unsigned* gd = &ghdr->gdone[b & 1];
-            if (__hip_atomic_load(gd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
-                const uint64_t tw = __builtin_amdgcn_s_memrealtime();
-                while (__hip_atomic_load(gd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
-                    if (__builtin_amdgcn_s_memrealtime() - tw > kWatchdogTicks) {
-                        __hip_atomic_fetch_or(L.watchdog, 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        return false;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-            }
-        }
-        PSGD_STAMP(st_gr += __builtin_amdgcn_s_memtime() - st_g;)
-        const float* grow = gring + gs * (kBlk * kBlk) + krow * kBlk;
-        const f32x4 g0 = *reinterpret_cast<const f32x4*>(grow);
-        const f32x4 g1 = *reinterpret_cast<const f32x4*>(grow + 4);
-        const float G[kBlk] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
         if constexpr (KEEP) {
-            // the block's rows are in registers (G and meta slots live until the next block's
-            // rows are handed back): free its ring slots
+            // the block's rows are in registers (its Gram and meta slots are reused only after
+            // the next block is handed back): free its ring slots
             __hip_atomic_store(&hdr->consumed, (unsigned)(t0 + kk), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-
         // p_k = x_k . W (one packed accumulator per row; eight rows interleave)
         PSGD_STAMP(const uint64_t st_a = __builtin_amdgcn_s_memtime();)
         float pk[kBlk];
@@ -385,6 +369,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         const float alpha = 1.0f - sv * lam;      // SquaredL2 shrink of this lane's row
         float z = reduce8(pk, lane);
         PSGD_STAMP(const uint64_t st_b = __builtin_amdgcn_s_memtime(); st_p += st_b - st_a;)
+        // the block's Gram triangle (Gram wave b&1 publishes blocks in order), waited for only
+        // now so that the dots above overlap its computation
+        PSGD_STAMP(const uint64_t st_g = __builtin_amdgcn_s_memtime();)
+        {
+            const unsigned need = (unsigned)(b >> 1) + 1;
+            unsigned* gd = &ghdr->gdone[b & 1];
+            if (__hip_atomic_load(gd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+                const uint64_t tw = __builtin_amdgcn_s_memrealtime();
+                while (__hip_atomic_load(gd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+                    if (__builtin_amdgcn_s_memrealtime() - tw > kWatchdogTicks) {
+                        __hip_atomic_fetch_or(L.watchdog, 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        return false;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+        }
+        PSGD_STAMP(st_gr += __builtin_amdgcn_s_memtime() - st_g;)
+        const float* grow = gring + gs * (kBlk * kBlk) + krow * kBlk;
+        const f32x4 g0 = *reinterpret_cast<const f32x4*>(grow);
+        const f32x4 g1 = *reinterpret_cast<const f32x4*>(grow + 4);
+        const float G[kBlk] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
 
         // the scalar recurrence: c_i from z_i, then every later row's dot moves by c_i G[k][i]
         // (SquaredL2 also shrinks the finished rows' z: zf keeps z_k for the loss)

@@ -1,0 +1,72 @@
+"""Summarise a tools/profile_round.sh output directory into one JSON for profiles/.
+
+Per kernel (matched by a name prefix): dispatches, average duration from the kernel trace, and
+per-dispatch averages of FETCH_SIZE / WRITE_SIZE / SQ_INSTS_* from the separate --pmc passes.
+HBM bytes follow MI355X_MICROARCH.md §HBM: rocprofv3 reports FETCH_SIZE and WRITE_SIZE in KiB,
+and on gfx950 FETCH_SIZE counts exactly half the bytes of a wide (16 B/lane) coalesced
+streaming read (global_load and LDS-DMA alike), so the read traffic is 2 x FETCH_SIZE x 1024.
+
+usage: python tools/pmc_summary.py <prof dir> <out.json> [--workload NAME]
+"""
+import argparse
+import csv
+import json
+import os
+import statistics
+
+KERNELS = ("psgd::chain_block", "psgd::chain_dense", "psgd::chain_general", "psgd::fold_kernel")
+
+
+def short(name):
+    for k in KERNELS:
+        if k in name:
+            return name[name.index(k):].split("(")[0]
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("prof")
+    ap.add_argument("out")
+    ap.add_argument("--workload", default="c2")
+    a = ap.parse_args()
+    out = {"workload": a.workload, "source": "rocprofv3 (tools/profile_round.sh)", "kernels": {}}
+    trace = os.path.join(a.prof, "trace", "run_kernel_trace.csv")
+    if os.path.exists(trace):
+        for r in csv.DictReader(open(trace)):
+            k = short(r["Kernel_Name"])
+            if not k:
+                continue
+            e = out["kernels"].setdefault(k, {"durations_ns": []})
+            e["durations_ns"].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    for sub in ("fetch", "write", "insts"):
+        path = os.path.join(a.prof, sub, "run_counter_collection.csv")
+        if not os.path.exists(path):
+            continue
+        for r in csv.DictReader(open(path)):
+            k = short(r["Kernel_Name"])
+            if not k:
+                continue
+            e = out["kernels"].setdefault(k, {"durations_ns": []})
+            e.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    for k, e in out["kernels"].items():
+        d = e.pop("durations_ns")
+        if d:
+            e["dispatches"] = len(d)
+            e["avg_duration_ms"] = statistics.mean(d) / 1e6
+        for c in list(e):
+            if isinstance(e[c], list):
+                e[c] = statistics.mean(e[c])
+        if "FETCH_SIZE" in e:
+            e["hbm_read_bytes"] = 2 * e["FETCH_SIZE"] * 1024   # gfx950 streaming-read correction
+        if "WRITE_SIZE" in e:
+            e["hbm_write_bytes"] = e["WRITE_SIZE"] * 1024
+        if "hbm_read_bytes" in e:
+            e["hbm_bytes"] = e["hbm_read_bytes"] + e.get("hbm_write_bytes", 0.0)
+    with open(a.out, "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+    print(json.dumps(out, indent=1, sort_keys=True))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Profiles of the bench workload for profiles/ (run on the GPU box through gpurun):
+#   1. kernel trace + stats (per-kernel durations)
+#   2. FETCH_SIZE pass, 3. WRITE_SIZE pass (separate --pmc runs; MI355X_MICROARCH.md §HBM)
+#   4. SQ instruction-mix pass (VALU vs MFMA vs LDS instructions)
+# Every GPU step has its own time limit; the script stops at the first failure.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/prof
+ARGS=${BENCH_ARGS:-"--no-cpu-baseline --steps 3 --warmup 1"}
+mkdir -p $OUT
+step() { echo "== $1"; shift; "$@"; rc=$?; echo "rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
+step trace timeout -k 10 240 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- python3 bench.py $ARGS
+step fetch timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/fetch -o run -- python3 bench.py $ARGS
+step write timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/write -o run -- python3 bench.py $ARGS
+step insts timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAVES -f csv -d $OUT/insts -o run -- python3 bench.py $ARGS
+find $OUT -name "*.csv" | sort
