@@ -36,6 +36,8 @@ namespace psgd {
 
 constexpr int kBlk = 8;           // rows per block
 constexpr int kPairs = 28;        // kBlk*(kBlk-1)/2 Gram entries below the diagonal
+constexpr float kNegLog2e = -1.44269504088896341f;   // u = -log2(e) * z
+constexpr float kLn2Neg = -0.693147180559945309f;    // z = -ln(2) * u
 static_assert(kMetaRows == 2 * kBlk, "a meta block holds two row blocks");
 
 struct GramHeader {
@@ -107,9 +109,9 @@ __device__ __forceinline__ float coef(float z, float y, float s, float ns, float
     if constexpr (GRAD == G_LEAST_SQUARES) {
         return __builtin_fmaf(ns, z, aux);            // aux = s*y: -s*z + s*y
     } else if constexpr (GRAD == G_LOGISTIC) {
-        const float e = __expf(-z);
-        const float sig = __builtin_amdgcn_rcpf(1.0f + e);
-        return ns * (sig - y);
+        // z is u = -log2(e) * dot: 1/(1+exp(-dot)) = 1/(1+2^u); aux = s*y
+        const float sig = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z));
+        return __builtin_fmaf(ns, sig, aux);
     } else {
         return (aux * z < 1.0f) ? s * aux : 0.0f;     // aux = ls = 2y - 1: -s * (-ls)
     }
@@ -264,7 +266,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             for (int q = 0; q < kPairs; ++q) g[q] = acc[q].x + acc[q].y;
 #pragma unroll
             for (int q = kPairs; q < 32; ++q) g[q] = 0.0f;
-            const float val = reduce32(g, lane);
+            float val = reduce32(g, lane);
+            if constexpr (GRAD == G_LOGISTIC) val *= kNegLog2e;   // the chain works on u
             float* slot = gring + gs * (kBlk * kBlk);
             gs += 2;
             if (gs >= GS) gs -= GS;
@@ -293,6 +296,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     const int krow = ((lane >> 5) & 1) | (((lane >> 4) & 1) << 1) | (((lane >> 3) & 1) << 2);
     const bool loss_lane = (lane & 7) == 0;   // one copy of every row's loss
+    // Logistic: the rows' margins go to L.zbuf and margin_loss_kernel sums their losses after
+    // the chain (log1pExp costs the sequential wave ~60 cycles per row; off its critical path)
+    constexpr bool LOSS_EXT = GRAD == G_LOGISTIC;
+    gmut<float> zout = as_global_mut(L.zbuf + (LOSS_EXT ? (int64_t)chain * L.zstride : 0));
     const float lam = float(kp.reg);
     double loss_sum = 0.0;
     float loss_blk = 0.0f;
@@ -363,11 +370,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         const float yv = float(meta.x), sv = float(meta.y);
         const float nsv = -sv;
         float aux;
-        if constexpr (GRAD == G_LEAST_SQUARES) aux = sv * yv;
-        else if constexpr (GRAD == G_HINGE) aux = 2.0f * yv - 1.0f;
-        else aux = 0.0f;
+        if constexpr (GRAD == G_HINGE) aux = 2.0f * yv - 1.0f;
+        else aux = sv * yv;
         const float alpha = 1.0f - sv * lam;      // SquaredL2 shrink of this lane's row
         float z = reduce8(pk, lane);
+        // Logistic runs the recurrence on u = -log2(e) z (its Gram triangle is scaled the same
+        // way by the Gram waves): exp(-z) is then one v_exp_f32 of u
+        if constexpr (GRAD == G_LOGISTIC) z *= kNegLog2e;
         PSGD_STAMP(const uint64_t st_b = __builtin_amdgcn_s_memtime(); st_p += st_b - st_a;)
         // the block's Gram triangle (Gram wave b&1 publishes blocks in order), waited for only
         // now so that the dots above overlap its computation
@@ -412,7 +421,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
         if constexpr (UPD != U_SQUARED_L2) zf = z;
         PSGD_STAMP(const uint64_t st_c = __builtin_amdgcn_s_memtime(); st_rec += st_c - st_b;)
-        {
+        if constexpr (LOSS_EXT) {
+            if (loss_lane && (!TAIL || krow < kk)) zout[t0 + krow] = zf * kLn2Neg;   // u -> dot
+        } else {
             const float l = row_loss<GRAD>(zf, yv, aux);
             if (loss_lane && (!TAIL || krow < kk)) loss_blk += l;
             if ((b & 3) == 3) { loss_sum += double(loss_blk); loss_blk = 0.0f; }
@@ -514,10 +525,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     if (lane == 0) {
         L.rv[chain] = rv;
-        L.loss[chain] = loss_sum;
+        if constexpr (!LOSS_EXT) L.loss[chain] = loss_sum;
         L.cnt[chain] = count;
         L.cnt_d[chain] = double(count);
     }
+}
+
+// The Logistic loss of the chain's rows from their margins (PSGD.scala:254's lossSum; [ext] MLlib
+// 1.6.1 LogisticGradient: margin = -z, loss = y > 0 ? log1pExp(margin) : log1pExp(margin) - margin),
+// in f64, one workgroup per chain. z_t is the fp32 chain's dot for row t before its update.
+__global__ __launch_bounds__(256) void margin_loss_kernel(ChainLaunch L) {
+    const int chain = blockIdx.x;
+    const int64_t n = L.cnt[chain];
+    const double* y = L.descs[chain].y;
+    const float* z = L.zbuf + (int64_t)chain * L.zstride;
+    double acc = 0.0;
+    for (int64_t t = threadIdx.x; t < n; t += blockDim.x) {
+        const double margin = -double(as_global(z)[t]);
+        const double l = log1p_exp(margin);
+        acc += as_global(y)[t] > 0.0 ? l : l - margin;
+    }
+    acc = wave_sum(acc);
+    __shared__ double part[4];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) L.loss[chain] = (part[0] + part[1]) + (part[2] + part[3]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -553,9 +585,15 @@ static int launch_block(const ChainLaunch& L, const KParams& kp, bool full, size
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
         hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(256), bytes, st, L, kp, g);
     }
+    if constexpr (GRAD == G_LOGISTIC) {
+        if (!L.zbuf) return (int)hipErrorInvalidValue;
+        hipLaunchKernelGGL(margin_loss_kernel, dim3(kp.n_chains), dim3(256), 0, st, L);
+    }
     return (int)hipGetLastError();
 }
 
+// The dispatch over every instantiation (left out of the diagnostic build, tools/chain_bench.hip).
+#ifndef PSGD_NO_DISPATCH
 template <typename S, int GRAD, int UPD>
 static int block_nv(const ChainLaunch& L, const KParams& kp, int64_t min_ld, int64_t max_ld,
                     size_t lds, hipStream_t st, int* variant) {
@@ -608,5 +646,7 @@ int launch_block_chains(const ChainLaunch& L, const KParams& kp, int storage, in
         return block_grad<float>(L, kp, gradient, updater, min_ld, max_ld, lds, stream, kernel_variant);
     return block_grad<double>(L, kp, gradient, updater, min_ld, max_ld, lds, stream, kernel_variant);
 }
+
+#endif  // PSGD_NO_DISPATCH
 
 }  // namespace psgd

@@ -87,7 +87,7 @@ struct psgd_ctx {
     std::mutex mu;
     std::map<int64_t, Part> parts;
     bool descs_dirty = true;
-    DevBuf descs, w_in, w_out, state, rv, loss, cnt_d, cnt, steps, partial, tmp, watchdog;
+    DevBuf descs, w_in, w_out, state, rv, loss, cnt_d, cnt, steps, partial, tmp, watchdog, zbuf;
     double steps_value = NAN;
     int64_t steps_n = 0;
     int32_t last_variant = 0;
@@ -263,7 +263,7 @@ int32_t psgd_ctx_destroy(psgd_ctx* ctx) {
         hipStreamSynchronize(ctx->stream);
         for (auto& kv : ctx->parts) free_part(kv.second);
         for (DevBuf* b : {&ctx->descs, &ctx->w_in, &ctx->w_out, &ctx->state, &ctx->rv, &ctx->loss,
-                          &ctx->cnt_d, &ctx->cnt, &ctx->steps, &ctx->partial, &ctx->tmp,
+                          &ctx->cnt_d, &ctx->cnt, &ctx->steps, &ctx->partial, &ctx->tmp, &ctx->zbuf,
                           &ctx->watchdog})
             b->release();
         if (ctx->ev_begin) hipEventDestroy(ctx->ev_begin);
@@ -472,6 +472,15 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
     L.steps = ctx->steps.as<double>();
     L.watchdog = ctx->watchdog.as<int>();
     L.stamps = nullptr;
+    L.zbuf = nullptr;
+    L.zstride = 0;
+    if (params->gradient == PSGD_GRADIENT_LOGISTIC && params->compute_dtype == PSGD_F32 &&
+        layout == psgd::kDense) {
+        // per-row margins of the fp32 Logistic block kernel (its loss is summed after the chain)
+        L.zstride = std::max<int64_t>(n_max, 1);
+        HIP_TRY(ctx->zbuf.ensure((size_t)P * (size_t)L.zstride * sizeof(float)));
+        L.zbuf = ctx->zbuf.as<float>();
+    }
     HIP_TRY(hipMemsetAsync(L.watchdog, 0, 16, st));
     psgd::KParams kp;
     kp.reg = params->reg_param;

@@ -284,6 +284,14 @@ __device__ __forceinline__ void lds_store_u32_asm(unsigned* p, unsigned v) {
 // the compiler does not drain the DMA before them; the depth is a compile-time constant (a
 // runtime s_waitcnt needs a branch tree that costs more than the row).
 // ------------------------------------------------------------------------------------------
+// Cache policy of the row stream's LDS-DMA loads (the aux operand of global_load_lds): nt (2).
+// Every row is read once per epoch and an epoch's rows (GBs) do not fit the caches, so nothing
+// is lost by not keeping them; measured on the c2 workload (tools/chain_bench, 256 chains, d 512):
+// 83.7-84.7 ns/row nt vs 85.7-87.2 default policy (LeastSquares), 93.4-93.7 vs 95.0-96.3 (Logistic).
+#ifndef PSGD_LOAD_AUX
+#define PSGD_LOAD_AUX 2
+#endif
+
 template <int NV>
 __host__ __device__ constexpr int loader_depth() {
     return NV == 1 ? 56 : NV == 2 ? 28 : NV == 4 ? 14 : 7;   // <= 56 instructions in vmcnt
@@ -323,7 +331,7 @@ __device__ __forceinline__ void ring_loader(const ChainLaunch& L, const ChainDes
             const V* src = (FULL || (v * 64 + lane) * VEC < ld) ? row + v * 64 + lane : row;
             __builtin_amdgcn_global_load_lds(
                 (const void*)(as_global(src)),
-                (__attribute__((address_space(3))) void*)(dst + v * 1024), 16, 0, 0);
+                (__attribute__((address_space(3))) void*)(dst + v * 1024), 16, 0, PSGD_LOAD_AUX);
         }
         slot = (slot + 1 == R) ? 0 : slot + 1;
     };

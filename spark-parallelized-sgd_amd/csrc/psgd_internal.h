@@ -41,6 +41,8 @@ struct ChainLaunch {
     const double* steps;     // [n_max] stepSize / sqrt(j), j = 1..n_max
     int* watchdog;           // set by a wave whose partner stopped making progress
     unsigned long long* stamps;  // per-wave cycle counters, diagnostic builds only (PSGD_STAMPS)
+    float* zbuf;             // [n_chains * zstride] per-row margins (fp32 Logistic block kernel)
+    int64_t zstride;
 };
 
 // Diagnostic builds (-DPSGD_STAMPS, tools/chain_bench.hip) count s_memtime cycles per wave.

@@ -5,6 +5,7 @@
 //   Gram waves: total, waiting for rows
 // Usage: chain_bench <rows per chain> <chains> <d> <grad 0|1|2> <upd 0|1>
 #define PSGD_STAMPS 1
+#define PSGD_NO_DISPATCH 1
 #include "../spark-parallelized-sgd_amd/csrc/psgd_block.hip"
 
 #include <stdio.h>
@@ -25,6 +26,20 @@ __global__ void fill(float* x, size_t n, unsigned seed) {
 __global__ void fill_d(double* x, size_t n, double v) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
         x[i] = v;
+}
+
+// only the f32 instantiations the bench shapes use (d = 256 / 512 / 1024: NV = 1 / 2 / 4, full rows)
+static int launch(const psgd::ChainLaunch& L, const psgd::KParams& kp, int grad, int upd, int d) {
+    const size_t lds = 160 * 1024 - 512;
+#define NVCASE(G, U)                                                                              \
+    if (grad == G && upd == U) {                                                                  \
+        if (d == 256) return psgd::launch_block<float, G, U, 1>(L, kp, true, lds, 0);             \
+        if (d == 512) return psgd::launch_block<float, G, U, 2>(L, kp, true, lds, 0);             \
+        if (d == 1024) return psgd::launch_block<float, G, U, 4>(L, kp, true, lds, 0);            \
+    }
+    NVCASE(0, 0) NVCASE(1, 0) NVCASE(0, 1) NVCASE(1, 1)
+#undef NVCASE
+    return -3;
 }
 
 int main(int argc, char** argv) {
@@ -59,6 +74,9 @@ int main(int argc, char** argv) {
     psgd::ChainLaunch L{};
     L.descs = dd; L.w_in = w_in; L.w_out = w_out; L.rv = rv; L.loss = loss; L.cnt_d = cnt_d;
     L.cnt = cnt; L.steps = steps; L.watchdog = wd; L.stamps = stamps;
+    float* zbuf;
+    CK(hipMalloc(&zbuf, (size_t)rows * P * 4));
+    L.zbuf = zbuf; L.zstride = rows;
     psgd::KParams kp{};
     kp.reg = 0.01; kp.d = d; kp.n_chains = P;
     hipEvent_t a, b;
@@ -67,7 +85,8 @@ int main(int argc, char** argv) {
     float best = 1e30f;
     for (int it = 0; it < 4; ++it) {
         CK(hipEventRecord(a));
-        int e = psgd::launch_block_chains(L, kp, 1, grad, upd, d, d, 160 * 1024 - 512, 0, &variant);
+        int e = launch(L, kp, grad, upd, d);
+        variant = 300 + d / 256;
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
         if (e) { fprintf(stderr, "launch failed %d\n", e); return 1; }
