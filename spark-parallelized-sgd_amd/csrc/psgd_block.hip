@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     __syncthreads();
 
     if (wave == 1) {
-        ring_loader<S, NV, FULL, kBlk>(L, dsc, hdr, meta_ring, ring, geom, lane);
+        ring_loader<S, NV, FULL, kBlk, kBlk>(L, dsc, hdr, meta_ring, ring, geom, lane, ghdr->gdone);
         return;
     }
 
@@ -341,7 +341,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             meta_ring + ms * kMetaBlockBytes + ((int)(b & 1) * kBlk + krow) * 16);
         if constexpr (KEEP) {
             // the block's rows are in registers (its Gram and meta slots are reused only after
-            // the next block is handed back): free its ring slots
+            // the next block is handed back): free its ring slots (the loader also waits for the
+            // block's Gram wave to be done with them)
             __hip_atomic_store(&hdr->consumed, (unsigned)(t0 + kk), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
         }

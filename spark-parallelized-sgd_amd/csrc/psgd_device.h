@@ -302,10 +302,13 @@ __device__ __forceinline__ void lds_store_u32_nowait(unsigned* p, unsigned v) {
     asm volatile("ds_write_b32 %0, %1" : : "v"(addr), "v"(v) : "memory");
 }
 
-template <typename S, int NV, bool FULL, int PUB>
+// GB > 0: rows are also read by two helper waves that take alternate blocks of GB rows and
+// count their finished blocks in gdone[0] (even blocks) / gdone[1] (odd blocks); a slot is free
+// only once both the consumer and its helper are done with it.
+template <typename S, int NV, bool FULL, int PUB, int GB = 0>
 __device__ __forceinline__ void ring_loader(const ChainLaunch& L, const ChainDesc& dsc, RingHeader* hdr,
                                             char* meta_ring, char* ring, const RingGeom& geom,
-                                            int lane) {
+                                            int lane, const unsigned* gdone = nullptr) {
     using V = typename Vec16<S>::type;
     constexpr int VEC = Vec16<S>::N;
     constexpr int ROW_BYTES = NV * 1024;
@@ -345,13 +348,21 @@ __device__ __forceinline__ void ring_loader(const ChainLaunch& L, const ChainDes
             // ring full: wait for the consumer to free slots. A ring deeper than the loader's
             // depth plus two groups always leaves the consumer published rows to work on; a
             // shallower one publishes everything issued first (drains the DMA).
-            if (R < D + 2 * PUB) {
+            // (the helper waves' next blocks, GB rows each, must be published too)
+            if (R < D + 2 * PUB + 2 * GB) {
                 asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
                 lds_store_u32_nowait(&hdr->ready, (unsigned)t);
             }
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             for (;;) {
-                const unsigned c = __builtin_amdgcn_readfirstlane(lds_load_u32_asm(&hdr->consumed));
+                unsigned c = __builtin_amdgcn_readfirstlane(lds_load_u32_asm(&hdr->consumed));
+                if constexpr (GB > 0) {
+                    const unsigned g0 = __builtin_amdgcn_readfirstlane(lds_load_u32_asm(&gdone[0]));
+                    const unsigned g1 = __builtin_amdgcn_readfirstlane(lds_load_u32_asm(&gdone[1]));
+                    // blocks 0 .. min(2 g0, 2 g1 + 1) - 1 are all done by their helper
+                    const unsigned gb = 2 * g0 < 2 * g1 + 1 ? 2 * g0 : 2 * g1 + 1;
+                    c = c < gb * GB ? c : gb * GB;
+                }
                 limit = (int64_t)c + R;
                 if (te <= limit) break;
                 if (__builtin_amdgcn_readfirstlane(lds_load_u32_asm(&hdr->stop))) goto drain;
