@@ -158,7 +158,7 @@ int32_t validate_params(const psgd_params* p) {
 }
 
 // Allocate per-chain buffers and upload descriptors (ctx->mu held).
-int32_t prepare(psgd_ctx* ctx, int32_t d, bool need_state, hipStream_t st) {
+int32_t prepare(psgd_ctx* ctx, int32_t d, int state_vectors, hipStream_t st) {
     const size_t P = ctx->parts.size();
     HIP_TRY(ctx->descs.ensure(std::max<size_t>(P, 1) * sizeof(psgd::ChainDesc)));
     HIP_TRY(ctx->w_in.ensure((size_t)std::max(d, 1) * sizeof(double)));
@@ -170,9 +170,9 @@ int32_t prepare(psgd_ctx* ctx, int32_t d, bool need_state, hipStream_t st) {
     HIP_TRY(ctx->partial.ensure(((size_t)std::max(d, 1) + 3) * sizeof(double)));
     HIP_TRY(ctx->tmp.ensure(((size_t)std::max(d, 1) + 8) * sizeof(double)));
     HIP_TRY(ctx->watchdog.ensure(16));
-    if (need_state)
-        HIP_TRY(ctx->state.ensure(std::max<size_t>(P, 1) * 2 * (size_t)std::max(d, 1) *
-                                  sizeof(double)));
+    if (state_vectors > 0)
+        HIP_TRY(ctx->state.ensure(std::max<size_t>(P, 1) * (size_t)state_vectors *
+                                  (size_t)std::max(d, 1) * sizeof(double)));
     if (ctx->descs_dirty) {
         std::vector<psgd::ChainDesc> h;
         h.reserve(P);
@@ -441,10 +441,10 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
     const int32_t layout = first.layout;
     const bool stateful = params->updater == PSGD_UPDATER_ADAGRAD || params->updater == PSGD_UPDATER_ADAM;
     const bool conv = params->convergence_tol > 0.0;
-    if (layout == psgd::kCsr && stateful)
-        return fail(PSGD_EUNSUPPORTED, "CSR rows with AdaGrad/Adam updaters are not built yet");
     const bool need_state = stateful || (layout == psgd::kCsr && conv);
-    rc = prepare(ctx, d, need_state, st);
+    // d-vectors of status per chain (chain_general: dense [SA|SB], CSR [SA|SB|SC])
+    const int state_vectors = !need_state ? 0 : layout == psgd::kCsr ? 3 : 2;
+    rc = prepare(ctx, d, state_vectors, st);
     if (rc) return rc;
     int64_t n_max = 0, max_ld = 0, min_ld = INT64_MAX;
     for (auto& kv : ctx->parts) {

@@ -282,10 +282,16 @@ __global__ __launch_bounds__(64) void chain_general(ChainLaunch L, KParams kp) {
     const gptr<int64_t> ROWP = as_global(dsc.row_ptr);
     const gptr<int32_t> COL = as_global(dsc.col);
     const gmut<double> W = as_global_mut(L.w_out + (int64_t)chain * d);
-    const gmut<double> SA = L.state ? as_global_mut(L.state + (int64_t)chain * 2 * d) : nullptr;
+    // per-chain status: dense rows [SA | SB] (2d), CSR rows [SA | SB | SC] (3d; SC: the sample's
+    // dense gradient for Adam, zero outside the row's indices between samples)
+    constexpr int NS = LAYOUT == kCsr ? 3 : 2;
+    const gmut<double> SA = L.state ? as_global_mut(L.state + (int64_t)chain * NS * d) : nullptr;
     const gmut<double> SB = L.state ? SA + d : nullptr;
+    const gmut<double> SC = (L.state && LAYOUT == kCsr) ? SA + 2 * d : nullptr;
 
     for (int i = lane; i < d; i += 64) W[i] = as_global(L.w_in)[i];
+    if constexpr (LAYOUT == kCsr && UPD == U_ADAM)
+        for (int i = lane; i < d; i += 64) SC[i] = 0.0;
     wave_mem_fence();
 
     double loss_sum = 0.0;
@@ -360,9 +366,52 @@ __global__ __launch_bounds__(64) void chain_general(ChainLaunch L, KParams kp) {
                         const double v = W[i];
                         W[i] = jsignum(v) * jmax(0.0, fabs(v) - shrink);
                     }
-                } else {
-                    static_assert(UPD == U_SQUARED_L2 || UPD == U_L1,
-                                  "CSR rows with a stateful updater are not built (EUNSUPPORTED)");
+                } else if constexpr (UPD == U_ADAGRAD) {
+                    // UPD.scala:199-227 on a gradient that is zero outside the row's indices:
+                    // the accumulator (None -> squaredGrad, i.e. zero there at the first sample)
+                    // and the weights change only at the row's indices (w + a*(0/..) == w)
+                    if (t == 0) {
+                        for (int i = lane; i < d; i += 64) SA[i] = 0.0;
+                        wave_mem_fence();
+                    }
+                    for (int64_t k = kb + lane; k < ke; k += 64) {
+                        const int i = COL[k];
+                        const double g = mult * double(X[k]);
+                        const double acc2 = SA[i] + g * g;
+                        SA[i] = acc2;
+                        const double old = W[i];
+                        const double nw = old + a * (g / sqrt(acc2 + 1.0));
+                        W[i] = nw;
+                        if constexpr (CONV) { const double df = old - nw; dsq += df * df; }
+                    }
+                    if constexpr (CONV) {
+                        wave_mem_fence();
+                        for (int i = lane; i < d; i += 64) nsq += W[i] * W[i];
+                    }
+                } else {  // U_ADAM, UPD.scala:252-285: v and r decay at every coordinate
+                    for (int64_t k = kb + lane; k < ke; k += 64) SC[COL[k]] = mult * double(X[k]);
+                    wave_mem_fence();
+                    const bool first = (t == 0);
+                    const double beta = kp.beta, gamma = kp.gamma;
+                    const double iter = double(t + 1);
+                    const double lr = s / (1.0 - pow(beta, iter));
+                    const double al = -lr;
+                    for (int i = lane; i < d; i += 64) {
+                        const double g = SC[i];
+                        const double sq = g * g;
+                        double v, r;
+                        if (first) { v = g * (1 - beta); r = sq * (1 - gamma); }
+                        else { v = SA[i] * beta + g * (1 - beta); r = SB[i] * gamma + sq * (1 - gamma); }
+                        SA[i] = v;
+                        SB[i] = r;
+                        const double fix1 = sqrt(1.0 - pow(r, iter)) + kp.eps;
+                        const double old = W[i];
+                        const double nw = old + al * (v / fix1);
+                        W[i] = nw;
+                        if constexpr (CONV) { const double df = old - nw; dsq += df * df; nsq += nw * nw; }
+                    }
+                    wave_mem_fence();
+                    for (int64_t k = kb + lane; k < ke; k += 64) SC[COL[k]] = 0.0;
                 }
                 if constexpr (CONV && (UPD == U_SQUARED_L2 || UPD == U_L1)) {
                     wave_mem_fence();
@@ -603,8 +652,7 @@ static int dispatch_layout(const ChainLaunch& L, const KParams& kp, int layout, 
         }
     }
     if (layout == kDense) return launch_gen<S, kDense, GRAD, UPD, CONV>(L, kp, st, variant);
-    if constexpr (UPD == U_ADAGRAD || UPD == U_ADAM) return -2;  // CSR + stateful: not built
-    else return launch_gen<S, kCsr, GRAD, UPD, CONV>(L, kp, st, variant);
+    return launch_gen<S, kCsr, GRAD, UPD, CONV>(L, kp, st, variant);
 }
 
 template <typename S, int GRAD, int UPD>

@@ -127,6 +127,34 @@ def main():
                 mat = O.Matrix(yr, row_ptr=rp, col=col, val=val, d=d)
                 cases.append(run_both(c, mat, py_partitions_csr(rp, col, val, yr, offs), offs))
 
+    # --- random CSR cases with the stateful updaters (appended: the cases above keep their data) ---
+    for g in GRAD:
+        for u in ("adagrad", "adam"):
+            for tol in (0.0, 0.01):
+                n, d = 120, 48
+                rp = [0]
+                col, val = [], []
+                for r in range(n):
+                    k = int(rng.integers(0, 7))
+                    idx = sorted(rng.choice(d, size=k, replace=False).tolist())
+                    col += idx
+                    val += list(map(float, rng.uniform(0, 1, size=k).round(6)))
+                    rp.append(len(col))
+                rp, col, val = np.array(rp), np.array(col, np.int32), np.array(val)
+                if g == "least_squares":
+                    # |g| < 1 keeps Adam's sqrt(1 - r^iter) real (see the dense Adam cases)
+                    yr = (rng.uniform(size=n) * 0.5).round(6)
+                    val = (0.3 * val).round(6)
+                else:
+                    yr = (rng.uniform(size=n) > 0.5).astype(float)
+                offs = [0, 40, 40, 120]  # includes an empty partition
+                c = dict(name=f"csr_{g}_{u}_tol{tol}", source="random", n=n, d=d, offsets=offs,
+                         gradient=g, updater=u, step=0.5, iters=3, reg=0.01, tol=tol,
+                         w0=[0.0] * d, row_ptr=rp.tolist(), col=col.tolist(), val=val.tolist(),
+                         y=yr.tolist())
+                mat = O.Matrix(yr, row_ptr=rp, col=col, val=val, d=d)
+                cases.append(run_both(c, mat, py_partitions_csr(rp, col, val, yr, offs), offs))
+
     out = os.path.join(HERE, "golden_cases.json")
     with open(out, "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py", "oracle": "oracle/psgd_oracle.c",

@@ -188,11 +188,31 @@ def test_fp32_compute_mode_tolerance(pkg, oracle, grad, d):
     assert_close(h, hr, rel=FP32_LOSS_REL, what="fp32 loss")
 
 
-def test_csr_stateful_updater_not_built(pkg):
-    data = pkg.PartitionedData.from_points([(1.0, ([0], [1.0], 3)), (0.0, ([2], [0.5], 3))], 1)
-    with pytest.raises(pkg.UnsupportedOperationException):
-        pkg.runParallelizedSGD(data, pkg.HingeGradient(), pkg.AdaGradSGDUpdater(), 1.0, 1, 0.0, 1.0,
-                               np.zeros(3), 0.0)
+def test_csr_stateful_updater(pkg, oracle):
+    # CSR rows with AdaGrad/Adam (UPD.scala:199-285 on a gradient that is zero outside the row's
+    # indices); the golden cases csr_*_adagrad/adam cover every gradient, this one a wide sparse d
+    rng = np.random.default_rng(11)
+    n, d = 90, 700
+    rp, col, val = [0], [], []
+    for _ in range(n):
+        idx = np.sort(rng.choice(d, size=int(rng.integers(1, 12)), replace=False))
+        col += idx.tolist()
+        val += rng.uniform(0, 1, size=len(idx)).tolist()
+        rp.append(len(col))
+    rp, col, val = np.array(rp), np.array(col, np.int32), np.array(val)
+    y = (rng.uniform(size=n) > 0.5).astype(float)
+    offs = [0, 30, 90]
+    parts = [pkg.CsrPartition(y[a:b], rp[a:b + 1] - rp[a], col[rp[a]:rp[b]], val[rp[a]:rp[b]], d)
+             for a, b in zip(offs[:-1], offs[1:])]
+    data = pkg.PartitionedData(parts)
+    for upd in ("adagrad", "adam"):
+        w, h, counts = pkg.runParallelizedSGD(data, pkg.HingeGradient(), getattr(pkg, U[upd])(), 0.5, 3,
+                                              0.0, 1.0, np.zeros(d), 0.0, return_chain_counts=True)
+        wr, hr, cr = oracle.run(oracle.Matrix(y, row_ptr=rp, col=col, val=val, d=d), offs, "hinge", upd,
+                                0.5, 3, 0.0, np.zeros(d), tol=0.0)
+        assert [list(map(int, c)) for c in counts] == [list(map(int, c)) for c in cr]
+        assert_close(w, wr, what=upd + " weights")
+        assert_close(h, hr, what=upd + " loss")
 
 
 def test_mini_batch_fraction(pkg):
