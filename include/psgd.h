@@ -69,7 +69,8 @@ typedef struct {
     int32_t iteration;          /* outer iteration i (1-based), sampling seed 42+i (PSGD:242) */
     double step_size;           /* stepSize > 0 */
     double reg_param;           /* regParam >= 0 */
-    double mini_batch_fraction; /* (0, 1]; only 1.0 is built (RDD.sample is then the identity) */
+    double mini_batch_fraction; /* [0, 1]: batch = RDD.sample(false, f, 42 + iteration) per
+                                   partition (BernoulliSampler [ext Spark 1.6.1]); 1 = every row */
     double convergence_tol;     /* [0, 1]; 0 disables the per-sample break (PSGD.scala:262) */
     double adam_beta, adam_gamma, adam_eps; /* AdamSGDUpdater(beta, gamma, eps), UPD:241-244 */
 } psgd_params;

@@ -34,6 +34,7 @@ class _Params(C.Structure):
         ("gradient", C.c_int32), ("updater", C.c_int32), ("step_size", C.c_double),
         ("reg_param", C.c_double), ("convergence_tol", C.c_double),
         ("adam_beta", C.c_double), ("adam_gamma", C.c_double), ("adam_eps", C.c_double),
+        ("mini_batch_fraction", C.c_double),
     ]
 
 
@@ -65,6 +66,11 @@ def lib():
         L.or_jrandom_gaussians.argtypes = [C.c_int64, C.c_int32, dp]
         L.or_initial_regval.argtypes = [C.c_int32, dp, C.POINTER(_Params)]
         L.or_initial_regval.restype = C.c_double
+        L.or_partition_seeds.argtypes = [C.c_int64, C.c_int32, i64p]
+        L.or_xorshift_hash_seed.argtypes = [C.c_int64]
+        L.or_xorshift_hash_seed.restype = C.c_int64
+        L.or_sample_partition.argtypes = [C.c_int64, C.c_int64, C.c_double, i32p]
+        L.or_sample_partition.restype = C.c_int64
         _lib = L
     return _lib
 
@@ -100,8 +106,10 @@ class Matrix:
         self.d = m.d
 
 
-def params(gradient, updater, step, reg=0.0, tol=0.001, beta=0.9, gamma=0.999, eps=1e-8):
+def params(gradient, updater, step, reg=0.0, tol=0.001, beta=0.9, gamma=0.999, eps=1e-8,
+           fraction=1.0):
     p = _Params()
+    p.mini_batch_fraction = fraction
     p.gradient = GRAD[gradient] if isinstance(gradient, str) else int(gradient)
     p.updater = UPD[updater] if isinstance(updater, str) else int(updater)
     p.step_size, p.reg_param, p.convergence_tol = step, reg, tol
@@ -111,7 +119,7 @@ def params(gradient, updater, step, reg=0.0, tol=0.001, beta=0.9, gamma=0.999, e
 
 def run(mat: Matrix, part_offsets, gradient, updater, step, iters, reg, w0, tol=0.001,
         groups=None, n_threads=1, **kw):
-    """ParallelizedSGD.runParallelizedSGD restated (miniBatchFraction = 1.0).
+    """ParallelizedSGD.runParallelizedSGD restated (fraction=... sets miniBatchFraction).
     Returns (weights, loss_history, chain_counts[iters_run, P])."""
     L = lib()
     offs = np.ascontiguousarray(part_offsets, dtype=np.int64)
@@ -158,6 +166,25 @@ def run_chains(mat: Matrix, part_offsets, gradient, updater, step, reg, w_in, to
     if rc != 0:
         raise RuntimeError("oracle or_run_chains failed")
     return w, rv, loss, cnt
+
+
+def partition_seeds(seed, P):
+    """PartitionwiseSampledRDD.getPartitions: java.util.Random(seed).nextLong() per partition."""
+    out = np.zeros(P, dtype=np.int64)
+    lib().or_partition_seeds(seed, P, out.ctypes.data_as(C.POINTER(C.c_int64)))
+    return out
+
+
+def xorshift_hash_seed(s):
+    return int(lib().or_xorshift_hash_seed(int(s)))
+
+
+def sample_partition(seed, n, fraction):
+    """BernoulliSampler(fraction) with setSeed(seed) over n rows: the selected row offsets."""
+    out = np.zeros(max(n, 1), dtype=np.int32)
+    m = lib().or_sample_partition(int(seed), int(n), float(fraction),
+                                  out.ctypes.data_as(C.POINTER(C.c_int32)))
+    return out[:m].copy()
 
 
 def generate_gd_input(offset, scale, n, seed):

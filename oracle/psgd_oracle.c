@@ -264,14 +264,17 @@ double or_initial_regval(int32_t d, const double* w, const or_params* prm) {
 /* ------------------------------------------------------------------------------------------
  * The chain -- ParallelizedSGD.scala:243-270.
  * ------------------------------------------------------------------------------------------ */
-int or_chain(const or_matrix* m, int64_t r0, int64_t r1, const or_params* prm,
-             const double* w_in, double* w_out, double* rv_out, double* loss_out,
-             int64_t* count_out) {
+/* The chain over rows r0 + k, k = 0..r1-r0-1, or over rows[k] (absolute row indices, the
+ * partition's sampled subsequence in iterator order) when rows is not null. */
+static int chain_rows(const or_matrix* m, int64_t r0, int64_t r1, const int32_t* rows,
+                      const or_params* prm, const double* w_in, double* w_out, double* rv_out,
+                      double* loss_out, int64_t* count_out) {
     int32_t d = m->d;
     size_t nd = (size_t)(d > 0 ? d : 1);
     int64_t max_nnz = 0;
     if (m->is_csr)
-        for (int64_t r = r0; r < r1; ++r) {
+        for (int64_t q = r0; q < r1; ++q) {
+            int64_t r = rows ? rows[q - r0] : q;
             int64_t z = m->row_ptr[r + 1] - m->row_ptr[r];
             if (z > max_nnz) max_nnz = z;
         }
@@ -298,7 +301,8 @@ int or_chain(const or_matrix* m, int64_t r0, int64_t r1, const or_params* prm,
     memset(&row, 0, sizeof(row));
     row.d = d;
     row.is_csr = m->is_csr;
-    for (int64_t r = r0; r < r1; ++r) {
+    for (int64_t q = r0; q < r1; ++q) {
+        const int64_t r = rows ? rows[q - r0] : q;
         if (m->is_csr) {
             int64_t b = m->row_ptr[r], e = m->row_ptr[r + 1];
             row.nnz = e - b;
@@ -321,6 +325,12 @@ int or_chain(const or_matrix* m, int64_t r0, int64_t r1, const or_params* prm,
     *count_out = count;
     free(buf);
     return 0;
+}
+
+int or_chain(const or_matrix* m, int64_t r0, int64_t r1, const or_params* prm,
+             const double* w_in, double* w_out, double* rv_out, double* loss_out,
+             int64_t* count_out) {
+    return chain_rows(m, r0, r1, NULL, prm, w_in, w_out, rv_out, loss_out, count_out);
 }
 
 /* ------------------------------------------------------------------------------------------
@@ -352,6 +362,8 @@ typedef struct {
     int64_t* cnt;
     int32_t tid, nthreads;
     int rc;
+    int32_t* const* rows;   /* sampled epoch: rows[p][0..nrows[p]) absolute row indices */
+    const int64_t* nrows;
 } chain_job;
 
 static void* chain_worker(void* arg) {
@@ -359,18 +371,23 @@ static void* chain_worker(void* arg) {
     int32_t d = jb->m->d;
     for (int32_t p = jb->tid; p < jb->P; p += jb->nthreads) {
         int64_t r0 = jb->offs[p], r1 = jb->offs[p + 1];
+        const int32_t* rows = NULL;
+        if (jb->rows) {
+            rows = jb->rows[p];
+            r1 = r0 + jb->nrows[p];
+        }
         if (jb->limits && r1 - r0 > jb->limits[p]) r1 = r0 + jb->limits[p];
-        if (or_chain(jb->m, r0, r1, jb->prm, jb->w_in, jb->w_out + (size_t)p * (size_t)d,
-                     &jb->rv[p], &jb->loss[p], &jb->cnt[p]) != 0)
+        if (chain_rows(jb->m, r0, r1, rows, jb->prm, jb->w_in, jb->w_out + (size_t)p * (size_t)d,
+                       &jb->rv[p], &jb->loss[p], &jb->cnt[p]) != 0)
             jb->rc = -1;
     }
     return NULL;
 }
 
-int or_run_chains(const or_matrix* m, int32_t P, const int64_t* part_offsets,
-                  const int64_t* part_limits, const or_params* prm, const double* w_in,
-                  double* w_out, double* rv_out, double* loss_out, int64_t* count_out,
-                  int32_t n_threads) {
+static int run_chains(const or_matrix* m, int32_t P, const int64_t* part_offsets,
+                      const int64_t* part_limits, int32_t* const* rows, const int64_t* nrows,
+                      const or_params* prm, const double* w_in, double* w_out, double* rv_out,
+                      double* loss_out, int64_t* count_out, int32_t n_threads) {
     if (n_threads < 1) n_threads = 1;
     if (n_threads > P) n_threads = P > 0 ? P : 1;
     chain_job* jobs = (chain_job*)calloc((size_t)n_threads, sizeof(chain_job));
@@ -378,7 +395,7 @@ int or_run_chains(const or_matrix* m, int32_t P, const int64_t* part_offsets,
     int rc = 0;
     for (int32_t t = 0; t < n_threads; ++t) {
         chain_job jb = {m, prm, P, part_offsets, part_limits, w_in, w_out, rv_out, loss_out,
-                        count_out, t, n_threads, 0};
+                        count_out, t, n_threads, 0, rows, nrows};
         jobs[t] = jb;
     }
     if (n_threads == 1) {
@@ -393,9 +410,18 @@ int or_run_chains(const or_matrix* m, int32_t P, const int64_t* part_offsets,
     return rc;
 }
 
+int or_run_chains(const or_matrix* m, int32_t P, const int64_t* part_offsets,
+                  const int64_t* part_limits, const or_params* prm, const double* w_in,
+                  double* w_out, double* rv_out, double* loss_out, int64_t* count_out,
+                  int32_t n_threads) {
+    return run_chains(m, P, part_offsets, part_limits, NULL, NULL, prm, w_in, w_out, rv_out,
+                      loss_out, count_out, n_threads);
+}
+
 /* ------------------------------------------------------------------------------------------
- * Driver -- ParallelizedSGD.scala:188-306 (miniBatchFraction == 1.0: RDD.sample with
- * fraction >= 1 is the identity on every partition [ext Spark 1.6.1 BernoulliSampler]).
+ * Driver -- ParallelizedSGD.scala:188-306. The batch of iteration i is
+ * data.sample(false, miniBatchFraction, 42 + i) (:242): or_sample_partition per partition with
+ * the seeds of or_partition_seeds(42 + i) (fraction >= 1: the identity; <= 0: empty).
  * ------------------------------------------------------------------------------------------ */
 int or_run(const or_matrix* m, int32_t P, const int64_t* part_offsets,
            const int32_t* group_offsets, int32_t n_groups,
@@ -430,9 +456,29 @@ int or_run(const or_matrix* m, int32_t P, const int64_t* part_offsets,
     int converged = 0;
     int32_t i = 1;
     int rc = 0;
+    const double frac = prm->mini_batch_fraction;
+    const int sampled = frac < 1.0;
+    int32_t** rows = NULL;
+    int64_t* nrows = NULL;
+    int64_t* pseeds = NULL;
+    if (sampled) {
+        rows = (int32_t**)calloc((size_t)(P > 0 ? P : 1), sizeof(int32_t*));
+        nrows = (int64_t*)calloc((size_t)(P > 0 ? P : 1), sizeof(int64_t));
+        pseeds = (int64_t*)calloc((size_t)(P > 0 ? P : 1), sizeof(int64_t));
+        for (int32_t p = 0; p < P; ++p)
+            rows[p] = (int32_t*)malloc(sizeof(int32_t) * (size_t)(part_offsets[p + 1] - part_offsets[p] + 1));
+    }
     while (!converged && i <= num_iterations) {  /* :237 */
-        rc = or_run_chains(m, P, part_offsets, NULL, prm, weights, cw, crv, closs, ccnt,
-                           n_threads);
+        if (sampled) {  /* :242 */
+            or_partition_seeds(42 + (int64_t)i, P, pseeds);
+            for (int32_t p = 0; p < P; ++p) {
+                const int64_t r0 = part_offsets[p];
+                nrows[p] = or_sample_partition(pseeds[p], part_offsets[p + 1] - r0, frac, rows[p]);
+                for (int64_t k = 0; k < nrows[p]; ++k) rows[p][k] += (int32_t)r0;
+            }
+        }
+        rc = run_chains(m, P, part_offsets, NULL, rows, nrows, prm, weights, cw, crv, closs, ccnt,
+                        n_threads);
         if (rc) break;
         if (chain_counts)
             for (int32_t p = 0; p < P; ++p) chain_counts[(size_t)(i - 1) * (size_t)P + p] = ccnt[p];
@@ -472,6 +518,12 @@ int or_run(const or_matrix* m, int32_t P, const int64_t* part_offsets,
         i += 1;
     }
     memcpy(w_out, weights, sizeof(double) * (size_t)d);
+    if (sampled) {
+        for (int32_t p = 0; p < P; ++p) free(rows[p]);
+        free(rows);
+        free(nrows);
+        free(pseeds);
+    }
     free(weights);
     free(prev);
     free(cw);
@@ -588,6 +640,96 @@ double or_fdlibm_log(double xin) {
     }
     if (k == 0) return f - s * (f - R);
     return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
+/* ------------------------------------------------------------------------------------------
+ * RDD.sample(withReplacement = false, fraction, seed) [ext Spark 1.6.1, restated from its
+ * published source]: PartitionwiseSampledRDD.getPartitions draws one seed per partition,
+ * in partition order, from java.util.Random(seed).nextLong(); compute() runs a clone of
+ * BernoulliSampler(fraction) with setSeed(that seed). Its RNG is XORShiftRandom, whose seed
+ * is hashSeed(s) = MurmurHash3.bytesHash(ByteBuffer.allocate(java.lang.Long.SIZE).putLong(s)
+ * .array()) [scala.util.hashing.MurmurHash3, Scala 2.10]: 64 bytes (Long.SIZE is in bits),
+ * s big-endian in the first 8, sign-extended from Int to Long. fraction <= 0: no rows;
+ * >= 1: every row; <= 0.4 (defaultMaxGapSamplingFraction): GapSamplingIterator (geometric
+ * skips, u = max(nextDouble, 5e-11), k = (int)(log(u) / log1p(-f)), one skip before the first
+ * row and one after every returned row); else the filter nextDouble() <= fraction per row.
+ * ------------------------------------------------------------------------------------------ */
+static int64_t jr_next_long(jrandom* r) {
+    int64_t hi = (int64_t)jr_next(r, 32);
+    int64_t lo = (int64_t)jr_next(r, 32);
+    return (int64_t)((uint64_t)hi << 32) + lo;
+}
+void or_partition_seeds(int64_t seed, int32_t P, int64_t* out) {
+    jrandom r;
+    jr_init(&r, seed);
+    for (int32_t p = 0; p < P; ++p) out[p] = jr_next_long(&r);
+}
+static uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+static uint32_t mm3_mix_last(uint32_t h, uint32_t k) {
+    k *= 0xcc9e2d51u;
+    k = rotl32(k, 15);
+    k *= 0x1b873593u;
+    return h ^ k;
+}
+int64_t or_xorshift_hash_seed(int64_t s) {
+    uint8_t bytes[64];
+    memset(bytes, 0, sizeof bytes);
+    for (int b = 0; b < 8; ++b) bytes[b] = (uint8_t)((uint64_t)s >> (56 - 8 * b));
+    uint32_t h = 0x3c074a61u;                     /* MurmurHash3.arraySeed */
+    for (int i = 0; i < 64; i += 4) {             /* no tail: 64 is a multiple of 4 */
+        uint32_t k = (uint32_t)bytes[i] | ((uint32_t)bytes[i + 1] << 8) |
+                     ((uint32_t)bytes[i + 2] << 16) | ((uint32_t)bytes[i + 3] << 24);
+        h = mm3_mix_last(h, k);
+        h = rotl32(h, 13);
+        h = h * 5u + 0xe6546b64u;
+    }
+    h ^= 64u;                                     /* finalizeHash(h, data.length) */
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    return (int64_t)(int32_t)h;
+}
+static int32_t xs_next(uint64_t* st, int bits) {
+    uint64_t x = *st;
+    x ^= x << 21;
+    x ^= x >> 35;   /* >>> on the Long */
+    x ^= x << 4;
+    *st = x;
+    return (int32_t)(x & ((1ULL << bits) - 1));
+}
+static double xs_next_double(uint64_t* st) {
+    int64_t a = (int64_t)xs_next(st, 26);
+    int64_t b = (int64_t)xs_next(st, 27);
+    return (double)((a << 27) + b) * 0x1.0p-53;
+}
+int64_t or_sample_partition(int64_t seed, int64_t n, double fraction, int32_t* rows_out) {
+    if (fraction <= 0.0) return 0;
+    int64_t m = 0;
+    if (fraction >= 1.0) {
+        for (int64_t t = 0; t < n; ++t) rows_out[m++] = (int32_t)t;
+        return m;
+    }
+    uint64_t st = (uint64_t)or_xorshift_hash_seed(seed);
+    if (fraction <= 0.4) {
+        const double lnq = log1p(-fraction);
+        int64_t pos = 0;
+        for (;;) {
+            double u = xs_next_double(&st);
+            if (u < 5e-11) u = 5e-11;          /* math.max(rng.nextDouble(), epsilon) */
+            const double q = log(u) / lnq;
+            const int64_t k = q >= 2147483647.0 ? 2147483647 : (int64_t)q;   /* Double.toInt */
+            pos += k;
+            if (pos >= n) break;
+            rows_out[m++] = (int32_t)pos;
+            pos += 1;
+        }
+    } else {
+        for (int64_t t = 0; t < n; ++t)
+            if (xs_next_double(&st) <= fraction) rows_out[m++] = (int32_t)t;
+    }
+    return m;
 }
 
 void or_jrandom_doubles(int64_t seed, int32_t n, double* out) {

@@ -61,6 +61,7 @@ typedef struct {
     double reg_param;
     double convergence_tol;
     double adam_beta, adam_gamma, adam_eps;
+    double mini_batch_fraction;   /* RDD.sample(false, f, 42 + i) per iteration (PSGD.scala:242) */
 } or_params;
 
 /* One chain (ParallelizedSGD.scala:243-270) over rows [r0, r1). */
@@ -78,7 +79,7 @@ int or_is_converged(int32_t d, const double* prev, const double* cur, double tol
 /* Updater regVal at iteration 0 (ParallelizedSGD.scala:231-233). */
 double or_initial_regval(int32_t d, const double* w, const or_params* prm);
 
-/* Full driver (ParallelizedSGD.scala:188-306) with miniBatchFraction == 1.0.
+/* Full driver (ParallelizedSGD.scala:188-306), prm->mini_batch_fraction sampling included.
  * part_offsets[P+1]: partition p holds rows [part_offsets[p], part_offsets[p+1]).
  * Returns number of loss-history entries in *n_hist (<= num_iterations).
  * chain_counts (nullable): [num_iterations * P], per-iteration per-chain processed counts.
@@ -94,6 +95,14 @@ int or_run_chains(const or_matrix* m, int32_t P, const int64_t* part_offsets,
                   const int64_t* part_limits, const or_params* prm, const double* w_in,
                   double* w_out /*[P*d]*/, double* rv_out, double* loss_out, int64_t* count_out,
                   int32_t n_threads);
+
+/* RDD.sample(false, fraction, seed) [ext Spark 1.6.1]: the per-partition seeds
+ * (java.util.Random(seed).nextLong() in partition order), XORShiftRandom.hashSeed, and the
+ * BernoulliSampler's row selection for one partition of n rows (returns the count, writes the
+ * selected row offsets 0..n-1 in iterator order). */
+void or_partition_seeds(int64_t seed, int32_t P, int64_t* out);
+int64_t or_xorshift_hash_seed(int64_t s);
+int64_t or_sample_partition(int64_t seed, int64_t n, double fraction, int32_t* rows_out);
 
 /* java.util.Random + StrictMath.log (fdlibm) restatements, for the suite's data generator
  * (ParallelizedSGDSuite.scala:42-62). */

@@ -329,12 +329,131 @@ def combine(a, b):
     w1, rv1, l1, c1 = a
     w2, rv2, l2, c2 = b
     s = float(c1 + c2)
-    w = [(w1[i] * float(c1) + w2[i] * float(c2)) / s for i in range(len(w1))]
-    return w, (rv1 * float(c1) + rv2 * float(c2)) / s, l1 + l2, c1 + c2
+    w = [_jdiv(w1[i] * float(c1) + w2[i] * float(c2), s) for i in range(len(w1))]
+    return w, _jdiv(rv1 * float(c1) + rv2 * float(c2), s), l1 + l2, c1 + c2
 
 
-def run(partitions, grad_kind, upd_kind, step, iters, reg, w0, tol=0.001, groups=None, **kw):
-    """PSGD:188-306 (miniBatchFraction == 1.0).  partitions: list of (rows, labels).
+def _jdiv(a: float, b: float) -> float:
+    """Java double division (IEEE 754: x/0 is +-Infinity or NaN, never an exception)."""
+    if b != 0.0:
+        return a / b
+    if a != a or a == 0.0:
+        return math.nan
+    return math.copysign(math.inf, a) * math.copysign(1.0, b)
+
+
+# ----------------------------------------------------------------------------- RDD.sample
+# [ext] Spark 1.6.1 RDD.sample(false, fraction, seed) -> PartitionwiseSampledRDD(BernoulliSampler),
+# restated from the published sources (not runnable here: no JVM): per-partition seeds from
+# java.util.Random(seed).nextLong() in partition order; BernoulliSampler.setSeed(s) seeds an
+# XORShiftRandom with hashSeed(s) = scala.util.hashing.MurmurHash3.bytesHash of the 64-byte
+# ByteBuffer.allocate(java.lang.Long.SIZE).putLong(s) (Int, sign-extended).
+
+M32 = 0xFFFFFFFF
+M64 = 0xFFFFFFFFFFFFFFFF
+
+
+def _rotl32(x, r):
+    return ((x << r) | (x >> (32 - r))) & M32
+
+
+def murmur3_bytes_hash(data: bytes, seed: int = 0x3C074A61) -> int:
+    """scala.util.hashing.MurmurHash3.bytesHash (MurmurHash3 x86_32), as a signed Int."""
+    def mix_last(h, k):
+        k = (k * 0xCC9E2D51) & M32
+        k = _rotl32(k, 15)
+        k = (k * 0x1B873593) & M32
+        return h ^ k
+    h = seed & M32
+    n4 = len(data) // 4
+    for i in range(n4):
+        k = data[4 * i] | (data[4 * i + 1] << 8) | (data[4 * i + 2] << 16) | (data[4 * i + 3] << 24)
+        h = mix_last(h, k)
+        h = _rotl32(h, 13)
+        h = (h * 5 + 0xE6546B64) & M32
+    tail = len(data) & 3
+    k = 0
+    i = 4 * n4
+    if tail == 3:
+        k ^= data[i + 2] << 16
+    if tail >= 2:
+        k ^= data[i + 1] << 8
+    if tail >= 1:
+        k ^= data[i]
+        h = mix_last(h, k)
+    h ^= len(data)
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & M32
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & M32
+    h ^= h >> 16
+    return h - (1 << 32) if h >= 1 << 31 else h
+
+
+def xorshift_hash_seed(s: int) -> int:
+    data = (s & M64).to_bytes(8, "big") + bytes(56)
+    return murmur3_bytes_hash(data)
+
+
+class XORShiftRandom:
+    """[ext] org.apache.spark.util.random.XORShiftRandom (1.6.1)."""
+
+    def __init__(self, seed: int):
+        self.seed = xorshift_hash_seed(seed) & M64
+
+    def next(self, bits: int) -> int:
+        x = self.seed
+        x ^= (x << 21) & M64
+        x ^= x >> 35
+        x ^= (x << 4) & M64
+        self.seed = x
+        return x & ((1 << bits) - 1)
+
+    def next_double(self) -> float:
+        return ((self.next(26) << 27) + self.next(27)) * (1.0 / (1 << 53))
+
+
+def partition_seeds(seed: int, P: int):
+    r = JavaRandom(seed)
+    out = []
+    for _ in range(P):
+        hi = r._next(32)
+        lo = r._next(32)
+        v = ((hi << 32) + lo) & M64
+        out.append(v - (1 << 64) if v >= 1 << 63 else v)
+    return out
+
+
+def bernoulli_sample(seed: int, n: int, fraction: float):
+    """BernoulliSampler(fraction).sample over n rows after setSeed(seed): the kept offsets."""
+    if fraction <= 0.0:
+        return []
+    if fraction >= 1.0:
+        return list(range(n))
+    rng = XORShiftRandom(seed)
+    out = []
+    if fraction <= 0.4:  # GapSamplingIterator, epsilon 5e-11
+        lnq = math.log1p(-fraction)
+        pos = 0
+        while True:
+            u = max(rng.next_double(), 5e-11)
+            q = math.log(u) / lnq
+            pos += 2147483647 if q >= 2147483647.0 else int(q)
+            if pos >= n:
+                break
+            out.append(pos)
+            pos += 1
+    else:
+        for t in range(n):
+            if rng.next_double() <= fraction:
+                out.append(t)
+    return out
+
+
+def run(partitions, grad_kind, upd_kind, step, iters, reg, w0, tol=0.001, groups=None,
+        fraction=1.0, **kw):
+    """PSGD:188-306, batch i = data.sample(false, fraction, 42 + i) (:242).
+    partitions: list of (rows, labels).
     groups: optional list of partition-index boundaries for the two-level combine tree.
     Returns (weights, loss_history, per-iteration chain counts)."""
     n = sum(len(p[1]) for p in partitions)
@@ -350,8 +469,15 @@ def run(partitions, grad_kind, upd_kind, step, iters, reg, w0, tol=0.001, groups
     P = len(partitions)
     bounds = groups if groups else [0, P]
     while not converged and i <= iters:
+        batch_parts = partitions
+        if fraction < 1.0:
+            seeds = partition_seeds(42 + i, P)
+            batch_parts = []
+            for (rows, labels), sd in zip(partitions, seeds):
+                keep = bernoulli_sample(sd, len(labels), fraction)
+                batch_parts.append(([rows[k] for k in keep], [labels[k] for k in keep]))
         res = [chain(rows, labels, grad_kind, upd_kind, step, reg, tol, weights, **kw)
-               for rows, labels in partitions]
+               for rows, labels in batch_parts]
         counts.append([r[3] for r in res])
         acc = None
         for gi in range(len(bounds) - 1):

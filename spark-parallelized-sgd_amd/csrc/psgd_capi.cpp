@@ -57,6 +57,54 @@ struct Part {
 };
 
 // Device buffer that only grows.
+// The seeds of RDD.sample(false, f, seed) [ext Spark 1.6.1]: PartitionwiseSampledRDD draws one
+// Long per partition, in partition order, from java.util.Random(seed); BernoulliSampler.setSeed
+// seeds its XORShiftRandom with hashSeed(s) = scala MurmurHash3.bytesHash of the 64-byte
+// ByteBuffer.allocate(java.lang.Long.SIZE).putLong(s) (Long.SIZE is in bits; an Int result,
+// sign-extended). The device walks the XORShift sequence (psgd_kernels.hip, sample_kernel).
+namespace sampling {
+struct JavaRandom {
+    uint64_t seed;
+    explicit JavaRandom(int64_t s) : seed(((uint64_t)s ^ 0x5DEECE66DULL) & ((1ULL << 48) - 1)) {}
+    int32_t next(int bits) {
+        seed = (seed * 0x5DEECE66DULL + 0xBULL) & ((1ULL << 48) - 1);
+        return (int32_t)(uint32_t)(seed >> (48 - bits));
+    }
+    int64_t next_long() {
+        const int64_t hi = next(32);
+        const int64_t lo = next(32);
+        return (int64_t)((uint64_t)hi << 32) + lo;
+    }
+};
+inline uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+inline int64_t xorshift_hash_seed(int64_t s) {
+    uint32_t h = 0x3c074a61u;   // MurmurHash3.arraySeed
+    for (int i = 0; i < 16; ++i) {
+        // little-endian words of the big-endian Long followed by 56 zero bytes
+        uint32_t k = 0;
+        if (i < 2) {
+            const uint64_t u = (uint64_t)s;
+            const int sh = 56 - 32 * i;   // byte b of the buffer is (s >> (56 - 8 b)) & 0xff
+            k = (uint32_t)((u >> sh) & 0xff) | ((uint32_t)((u >> (sh - 8)) & 0xff) << 8) |
+                ((uint32_t)((u >> (sh - 16)) & 0xff) << 16) | ((uint32_t)((u >> (sh - 24)) & 0xff) << 24);
+        }
+        k *= 0xcc9e2d51u;
+        k = rotl32(k, 15);
+        k *= 0x1b873593u;
+        h ^= k;
+        h = rotl32(h, 13);
+        h = h * 5u + 0xe6546b64u;
+    }
+    h ^= 64u;
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    return (int64_t)(int32_t)h;
+}
+}  // namespace sampling
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -88,6 +136,7 @@ struct psgd_ctx {
     std::map<int64_t, Part> parts;
     bool descs_dirty = true;
     DevBuf descs, w_in, w_out, state, rv, loss, cnt_d, cnt, steps, partial, tmp, watchdog, zbuf;
+    DevBuf sdescs, srows, sys, xstate;   // sampled epochs (miniBatchFraction < 1)
     double steps_value = NAN;
     int64_t steps_n = 0;
     int32_t last_variant = 0;
@@ -150,10 +199,6 @@ int32_t validate_params(const psgd_params* p) {
                  p->mini_batch_fraction);
         return fail(PSGD_EINVAL, buf);
     }
-    if (p->mini_batch_fraction > eps && p->mini_batch_fraction < 1.0 - eps)
-        return fail(PSGD_EUNSUPPORTED,
-                    "miniBatchFraction < 1.0 (Bernoulli sampling, ParallelizedSGD.scala:242) is "
-                    "not built yet");
     return PSGD_OK;
 }
 
@@ -185,6 +230,7 @@ int32_t prepare(psgd_ctx* ctx, int32_t d, int state_vectors, hipStream_t st) {
             c.col = q.col;
             c.n_rows = q.n_rows;
             c.ld = q.ld;
+            c.rows = nullptr;   // every row (sampled epochs get descriptors of their own)
             h.push_back(c);
         }
         if (P) {
@@ -264,6 +310,7 @@ int32_t psgd_ctx_destroy(psgd_ctx* ctx) {
         for (auto& kv : ctx->parts) free_part(kv.second);
         for (DevBuf* b : {&ctx->descs, &ctx->w_in, &ctx->w_out, &ctx->state, &ctx->rv, &ctx->loss,
                           &ctx->cnt_d, &ctx->cnt, &ctx->steps, &ctx->partial, &ctx->tmp, &ctx->zbuf,
+                          &ctx->sdescs, &ctx->srows, &ctx->sys, &ctx->xstate,
                           &ctx->watchdog})
             b->release();
         if (ctx->ev_begin) hipEventDestroy(ctx->ev_begin);
@@ -455,13 +502,42 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         }
     }
     if (max_ld == 0) max_ld = min_ld = d;
-    const bool sample_empty = params->mini_batch_fraction <= 1e-6;
+    // RDD.sample(false, f, 42 + i) (PSGD.scala:242) [ext Spark 1.6.1 BernoulliSampler]:
+    // f <= 0 gives every partition empty, f >= 1 every row, else a Bernoulli batch per partition
+    const bool sample_empty = params->mini_batch_fraction <= 0.0;
+    const bool sampled = !sample_empty && params->mini_batch_fraction < 1.0;
     rc = ensure_steps(ctx, params->step_size, n_max, st);
     if (rc) return rc;
 
     const int P = (int)ctx->parts.size();
     psgd::ChainLaunch L;
     L.descs = ctx->descs.as<psgd::ChainDesc>();
+    if (sampled) {
+        // one XORShiftRandom per partition, seeded as PartitionwiseSampledRDD does: the p-th
+        // java.util.Random(42 + i).nextLong() for partition index p, through hashSeed
+        std::vector<uint64_t> xs((size_t)P);
+        sampling::JavaRandom jr(42 + (int64_t)params->iteration);
+        int64_t drawn = 0, s = 0;
+        size_t c = 0;
+        for (auto& kv : ctx->parts) {
+            while (drawn <= kv.first) { s = jr.next_long(); ++drawn; }
+            xs[c++] = (uint64_t)sampling::xorshift_hash_seed(s);
+        }
+        const int64_t stride = std::max<int64_t>(n_max, 1);
+        HIP_TRY(ctx->sdescs.ensure((size_t)P * sizeof(psgd::ChainDesc)));
+        HIP_TRY(ctx->srows.ensure((size_t)P * (size_t)stride * sizeof(int32_t)));
+        HIP_TRY(ctx->sys.ensure((size_t)P * (size_t)stride * sizeof(double)));
+        HIP_TRY(ctx->xstate.ensure((size_t)P * sizeof(uint64_t)));
+        HIP_TRY(hipMemcpyAsync(ctx->xstate.p, xs.data(), (size_t)P * sizeof(uint64_t),
+                               hipMemcpyHostToDevice, st));
+        int e = psgd::launch_sample(L.descs, ctx->sdescs.as<psgd::ChainDesc>(),
+                                    ctx->xstate.as<uint64_t>(), params->mini_batch_fraction,
+                                    ctx->srows.as<int32_t>(), ctx->sys.as<double>(), stride, P, st);
+        if (e) return fail(PSGD_EDEVICE, "sample kernel launch failed");
+        // host data may be freed by the caller once run_epoch returns: wait for the copy
+        HIP_TRY(hipStreamSynchronize(st));
+        L.descs = ctx->sdescs.as<psgd::ChainDesc>();
+    }
     L.w_in = d_w_in;
     L.w_out = ctx->w_out.as<double>();
     L.state = need_state ? ctx->state.as<double>() : nullptr;

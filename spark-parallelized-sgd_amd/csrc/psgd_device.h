@@ -324,9 +324,13 @@ __device__ __forceinline__ void ring_loader(const ChainLaunch& L, const ChainDes
     const int mrow = lane >> 2;
     int64_t limit = R;            // rows < limit have a free slot
     int slot = 0, mslot = 0;
+    // sampled epoch: sample t is row rows[t], read with scalar loads (constant address space)
+    const int32_t __attribute__((address_space(4)))* RIDX =
+        (const int32_t __attribute__((address_space(4)))*)dsc.rows;
     auto issue_row = [&](int64_t t) __attribute__((always_inline)) {
         char* dst = ring + slot * ROW_BYTES;
-        const V* row = reinterpret_cast<const V*>(X + t * ld);
+        const int64_t r = RIDX ? (int64_t)RIDX[t] : t;
+        const V* row = reinterpret_cast<const V*>(X + r * ld);
         // every lane issues (past the row end it re-reads the row's first vector, bytes the
         // consumers ignore): each row is exactly NV vmcnt entries, which the counted waits need
 #pragma unroll

@@ -14,6 +14,8 @@ struct ChainDesc {
     const int32_t* col;      // CSR column indices
     int64_t n_rows;
     int64_t ld;              // dense: leading dimension in elements (>= d, multiple of 16B/elt)
+    const int32_t* rows;     // sampled epoch: the chain's t-th sample is partition row rows[t]
+                             // (y is then the sampled rows' labels); null: row t
 };
 
 // Per-launch scalars (hyper-parameters of ParallelizedSGD, PSGD.scala:46-50).
@@ -69,5 +71,11 @@ int launch_fold(const double* w, int64_t w_stride, const double* rv, const doubl
                 const int* watchdog, hipStream_t stream);
 int launch_sq_terms(const double* a, const double* b, int d, double* out2, hipStream_t stream);
 int launch_steps(double step, int64_t n, double* steps, hipStream_t stream);
+// RDD.sample(false, fraction, seed) per partition (PSGD.scala:242): from the registered
+// descriptors `base`, the epoch's descriptors `out` (rows/y/n_rows of the sampled subsequence;
+// rows and labels in `rows`/`ys`, `stride` entries per chain). xs_state[c] is the chain's
+// XORShiftRandom state (hashSeed of its partition seed, computed by the host).
+int launch_sample(const ChainDesc* base, ChainDesc* out, const uint64_t* xs_state, double fraction,
+                  int32_t* rows, double* ys, int64_t stride, int n_chains, hipStream_t stream);
 
 }  // namespace psgd

@@ -304,12 +304,13 @@ __global__ __launch_bounds__(64) void chain_general(ChainLaunch L, KParams kp) {
         int64_t kb = 0, ke = 0;
         // dot(data, weights)
         double acc = 0.0;
+        const int64_t ri = dsc.rows ? (int64_t)as_global(dsc.rows)[t] : t;   // sampled epoch
         if constexpr (LAYOUT == kDense) {
-            xr = X + t * dsc.ld;
+            xr = X + ri * dsc.ld;
             for (int i = lane; i < d; i += 64) acc = m_fma(double(xr[i]), W[i], acc);
         } else {
-            kb = ROWP[t];
-            ke = ROWP[t + 1];
+            kb = ROWP[ri];
+            ke = ROWP[ri + 1];
             for (int64_t k = kb + lane; k < ke; k += 64)
                 acc = m_fma(double(X[k]), W[COL[k]], acc);
         }
@@ -720,6 +721,78 @@ int launch_fold(const double* w, int64_t w_stride, const double* rv, const doubl
 
 int launch_sq_terms(const double* a, const double* b, int d, double* out2, hipStream_t stream) {
     hipLaunchKernelGGL(sq_terms_kernel, dim3(1), dim3(256), 0, stream, a, b, d, out2);
+    return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// Bernoulli sampling of one epoch's batch ([ext] Spark 1.6.1 BernoulliSampler on an
+// XORShiftRandom, restated in oracle/psgd_oracle.c or_sample_partition): one lane per chain
+// walks its partition in iterator order. fraction <= 0.4: GapSamplingIterator (geometric skips,
+// u = max(nextDouble, 5e-11), k = (int)(log(u) / log1p(-f)), a skip before the first row and
+// after every returned row); else the filter nextDouble() <= fraction.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int32_t xs_next(uint64_t& st, int bits) {
+    uint64_t x = st;
+    x ^= x << 21;
+    x ^= x >> 35;
+    x ^= x << 4;
+    st = x;
+    return (int32_t)(x & ((1ull << bits) - 1));
+}
+__device__ __forceinline__ double xs_next_double(uint64_t& st) {
+    const int64_t a = xs_next(st, 26);
+    const int64_t b = xs_next(st, 27);
+    return (double)((a << 27) + b) * 0x1.0p-53;
+}
+
+__global__ __launch_bounds__(64) void sample_kernel(const ChainDesc* __restrict__ base,
+                                                    ChainDesc* __restrict__ out,
+                                                    const uint64_t* __restrict__ xs_state,
+                                                    double fraction, int32_t* __restrict__ rows,
+                                                    double* __restrict__ ys, int64_t stride, int n) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    ChainDesc dsc = base[c];
+    uint64_t st = xs_state[c];
+    int32_t* r = rows + (int64_t)c * stride;
+    double* yo = ys + (int64_t)c * stride;
+    const gptr<double> Y = as_global(dsc.y);
+    const int64_t nr = dsc.n_rows;
+    int64_t m = 0;
+    if (fraction <= 0.4) {
+        const double lnq = log1p(-fraction);
+        int64_t pos = 0;
+        for (;;) {
+            double u = xs_next_double(st);
+            if (u < 5e-11) u = 5e-11;
+            const double q = log(u) / lnq;
+            pos += q >= 2147483647.0 ? 2147483647 : (int64_t)q;
+            if (pos >= nr) break;
+            r[m] = (int32_t)pos;
+            yo[m] = Y[pos];
+            ++m;
+            pos += 1;
+        }
+    } else {
+        for (int64_t t = 0; t < nr; ++t) {
+            if (xs_next_double(st) <= fraction) {
+                r[m] = (int32_t)t;
+                yo[m] = Y[t];
+                ++m;
+            }
+        }
+    }
+    dsc.rows = r;
+    dsc.y = yo;
+    dsc.n_rows = m;
+    out[c] = dsc;
+}
+
+int launch_sample(const ChainDesc* base, ChainDesc* out, const uint64_t* xs_state, double fraction,
+                  int32_t* rows, double* ys, int64_t stride, int n_chains, hipStream_t stream) {
+    if (n_chains <= 0) return 0;
+    hipLaunchKernelGGL(sample_kernel, dim3((unsigned)((n_chains + 63) / 64)), dim3(64), 0, stream,
+                       base, out, xs_state, fraction, rows, ys, stride, n_chains);
     return (int)hipGetLastError();
 }
 

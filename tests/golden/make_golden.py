@@ -46,13 +46,15 @@ def py_partitions_csr(rp, col, val, y, offs):
 
 
 def run_both(case, mat, py_parts, offs):
-    kw = dict(tol=case["tol"])
+    frac = case.get("fraction", 1.0)
+    kw = dict(tol=case["tol"], fraction=frac)
     w, h, c = O.run(mat, offs, case["gradient"], case["updater"], case["step"], case["iters"],
                     case["reg"], np.array(case["w0"]), **kw)
     wp, hp, cp = R.run(py_parts, GRAD[case["gradient"]], UPD[case["updater"]], case["step"],
-                       case["iters"], case["reg"], list(case["w0"]), tol=case["tol"])
-    assert list(map(float, w)) == wp, (case["name"], "weights differ between C and Python")
-    assert list(map(float, h)) == hp, (case["name"], "loss history differs")
+                       case["iters"], case["reg"], list(case["w0"]), tol=case["tol"], fraction=frac)
+    same = lambda a, b: len(a) == len(b) and all(x == y or (x != x and y != y) for x, y in zip(a, b))
+    assert same(list(map(float, w)), wp), (case["name"], "weights differ between C and Python")
+    assert same(list(map(float, h)), hp), (case["name"], "loss history differs")
     assert [list(map(int, r)) for r in c[:len(cp)]] == cp, (case["name"], "counts differ")
     case["expected"] = {"weights": [float(v) for v in w], "loss_history": [float(v) for v in h],
                         "chain_counts": [list(map(int, r)) for r in c[:len(h) if len(h) else 0]]}
@@ -154,6 +156,42 @@ def main():
                          y=yr.tolist())
                 mat = O.Matrix(yr, row_ptr=rp, col=col, val=val, d=d)
                 cases.append(run_both(c, mat, py_partitions_csr(rp, col, val, yr, offs), offs))
+
+    # --- miniBatchFraction < 1: RDD.sample(false, f, 42 + i) per iteration (PSGD.scala:242) ---
+    for g, u, frac, tol in (("logistic", "simple", 0.3, 0.0), ("logistic", "squared_l2", 0.7, 0.0),
+                            ("least_squares", "simple", 0.05, 0.0), ("hinge", "l1", 0.5, 0.01),
+                            ("logistic", "adagrad", 0.2, 0.0), ("least_squares", "squared_l2", 0.9, 0.001),
+                            ("hinge", "simple", 0.02, 0.0)):
+        n, d = 400, 6
+        Xr = rng.standard_normal((n, d)).round(6)
+        wt = rng.standard_normal(d)
+        if g == "least_squares":
+            yr = (Xr @ wt + 0.1 * rng.standard_normal(n)).round(6)
+        else:
+            yr = ((Xr @ wt + rng.logistic(size=n)) > 0).astype(float)
+        offs = [0, 250, 251, 251, 400]   # a one-row and an empty partition
+        c = dict(name=f"sampled_{g}_{u}_f{frac}_tol{tol}", source="random", n=n, d=d, offsets=offs,
+                 gradient=g, updater=u, step=0.05 if g == "least_squares" else 0.5, iters=6,
+                 reg=0.01, tol=tol, fraction=frac,
+                 w0=list(map(float, (0.1 * rng.standard_normal(d)).round(6))),
+                 X=Xr.tolist(), y=yr.tolist())
+        cases.append(run_both(c, O.Matrix(yr, Xr), py_partitions_dense(Xr, yr, offs), offs))
+    for g, u, frac in (("hinge", "simple", 0.25), ("logistic", "adam", 0.6)):
+        n, d = 200, 40
+        rp, col, val = [0], [], []
+        for r in range(n):
+            k = int(rng.integers(0, 8))
+            col += sorted(rng.choice(d, size=k, replace=False).tolist())
+            val += list(map(float, rng.uniform(0, 1, size=k).round(6)))
+            rp.append(len(col))
+        rp, col, val = np.array(rp), np.array(col, np.int32), np.array(val)
+        yr = (rng.uniform(size=n) > 0.5).astype(float)
+        offs = [0, 90, 200]
+        c = dict(name=f"sampled_csr_{g}_{u}_f{frac}", source="random", n=n, d=d, offsets=offs,
+                 gradient=g, updater=u, step=0.5, iters=4, reg=0.01, tol=0.0, fraction=frac,
+                 w0=[0.0] * d, row_ptr=rp.tolist(), col=col.tolist(), val=val.tolist(), y=yr.tolist())
+        mat = O.Matrix(yr, row_ptr=rp, col=col, val=val, d=d)
+        cases.append(run_both(c, mat, py_partitions_csr(rp, col, val, yr, offs), offs))
 
     out = os.path.join(HERE, "golden_cases.json")
     with open(out, "w") as f:

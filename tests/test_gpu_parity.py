@@ -65,8 +65,9 @@ def data_for(pkg, oracle, case):
 def run_case(pkg, data, case, **kw):
     g = getattr(pkg, G[case["gradient"]])()
     u = getattr(pkg, U[case["updater"]])()
-    return pkg.runParallelizedSGD(data, g, u, case["step"], case["iters"], case["reg"], 1.0,
-                                  np.array(case["w0"]), case["tol"], return_chain_counts=True, **kw)
+    return pkg.runParallelizedSGD(data, g, u, case["step"], case["iters"], case["reg"],
+                                  case.get("fraction", 1.0), np.array(case["w0"]), case["tol"],
+                                  return_chain_counts=True, **kw)
 
 
 def test_golden_cases_fp64(pkg, oracle, golden):
@@ -215,13 +216,32 @@ def test_csr_stateful_updater(pkg, oracle):
         assert_close(h, hr, what=upd + " loss")
 
 
-def test_mini_batch_fraction(pkg):
+def test_mini_batch_fraction(pkg, oracle):
+    """miniBatchFraction < 1: batch i = data.sample(false, f, 42 + i) (PSGD.scala:242) through
+    the fp32 block kernel and the per-sample kernels (the fp64 path is in the golden cases);
+    both branches of the sampler (gap sampling f <= 0.4, the filter above)."""
     rng = np.random.default_rng(2)
-    X, y = synth(rng, 100, 8, "logistic")
-    data = pkg.PartitionedData.parallelize(y, X, 2)
-    with pytest.raises(pkg.UnsupportedOperationException):
-        pkg.runParallelizedSGD(data, pkg.LogisticGradient(), pkg.SimpleSGDUpdater(), 1.0, 1, 0.0, 0.5,
-                               np.zeros(8), 0.0)
+    X, y = synth(rng, 3000, 64, "logistic")
+    offs = [0, 1000, 1001, 2000, 3000]
+    parts = [pkg.DensePartition(y[a:b], X[a:b]) for a, b in zip(offs[:-1], offs[1:])]
+    data = pkg.PartitionedData(parts)
+    for frac in (0.1, 0.75):
+        # fp64 per-sample kernel (dense d = 64 fits the LDS-ring kernel)
+        w, h, counts = pkg.runParallelizedSGD(data, pkg.LogisticGradient(), pkg.SimpleSGDUpdater(), 0.5, 4,
+                                              0.0, frac, np.zeros(64), 0.0, return_chain_counts=True)
+        wr, hr, cr = oracle.run(oracle.Matrix(y, X), offs, "logistic", "simple", 0.5, 4, 0.0, np.zeros(64),
+                                tol=0.0, fraction=frac)
+        assert [list(map(int, c)) for c in counts] == [list(map(int, c)) for c in cr]
+        assert 0 < cr[0][0] < 1000
+        assert_close(w, wr, what=f"f={frac} weights")
+        assert_close(h, hr, what=f"f={frac} loss")
+        # fp32 block kernel: same batches, the fp32 tolerance
+        w, h = pkg.runParallelizedSGD(data, pkg.LogisticGradient(), pkg.SimpleSGDUpdater(), 0.01, 4, 0.0,
+                                      frac, np.zeros(64), 0.0, compute_dtype="f32")
+        wr, hr, _ = oracle.run(oracle.Matrix(y, X.astype(np.float64)), offs, "logistic", "simple", 0.01, 4,
+                               0.0, np.zeros(64), tol=0.0, fraction=frac)
+        assert np.max(np.abs(w - wr)) <= FP32_REL * np.max(np.abs(wr))
+        assert_close(h, hr, rel=FP32_LOSS_REL, what="fp32 loss")
 
 
 def test_empty_partitions_nan_poisoning(pkg, oracle):

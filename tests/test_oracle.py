@@ -133,7 +133,40 @@ def test_golden_fixtures_reproduce(oracle, golden):
             m = oracle.Matrix(np.array(case["y"]), row_ptr=np.array(case["row_ptr"]),
                               col=np.array(case["col"]), val=np.array(case["val"]), d=case["d"])
         w, h, c = oracle.run(m, case["offsets"], case["gradient"], case["updater"], case["step"],
-                             case["iters"], case["reg"], np.array(case["w0"]), tol=case["tol"])
+                             case["iters"], case["reg"], np.array(case["w0"]), tol=case["tol"],
+                             fraction=case.get("fraction", 1.0))
         e = case["expected"]
         assert list(map(float, w)) == e["weights"], case["name"]
         assert list(map(float, h)) == e["loss_history"], case["name"]
+
+
+def test_murmur3_published_vectors():
+    """XORShiftRandom.hashSeed's MurmurHash3 (scala.util.hashing.MurmurHash3.bytesHash, the
+    x86_32 algorithm) against the algorithm's published test vectors."""
+    import psgd_ref as R
+    vec = [(b"", 0, 0), (b"", 1, 0x514E28B7), (b"", 0xFFFFFFFF, 0x81F16F39), (b"\0\0\0\0", 0, 0x2362F9DE),
+           (b"\x21\x43\x65\x87", 0, 0xF55B516B), (b"\x21\x43\x65\x87", 0x5082EDEE, 0x2362F9DE),
+           (b"\x21\x43\x65", 0, 0x7E4A8634), (b"\x21\x43", 0, 0xA0F7B07A), (b"\x21", 0, 0x72661CF4),
+           (b"\xff\xff\xff\xff", 0, 0x76293B50), (b"\0\0\0", 0, 0x85F0B427), (b"\0\0", 0, 0x30F4C306)]
+    for data, seed, want in vec:
+        assert R.murmur3_bytes_hash(data, seed) & 0xFFFFFFFF == want, (data, seed)
+
+
+def test_sampler_c_and_python_agree(oracle):
+    """RDD.sample(false, f, seed) restated twice: the C oracle and the pure-Python one select the
+    same rows (java.util.Random(42).nextLong() = -5025562857975149833, the JDK's known value)."""
+    import psgd_ref as R
+    assert int(oracle.partition_seeds(42, 1)[0]) == -5025562857975149833
+    rng = np.random.default_rng(5)
+    for s in rng.integers(-2**63, 2**63 - 1, 40):
+        assert R.xorshift_hash_seed(int(s)) == oracle.xorshift_hash_seed(int(s))
+    assert R.partition_seeds(43, 7) == [int(v) for v in oracle.partition_seeds(43, 7)]
+    for f in (1e-6, 0.01, 0.2, 0.4, 0.400001, 0.6, 0.999, 1.0, 0.0):
+        for sd in oracle.partition_seeds(44, 3):
+            a = R.bernoulli_sample(int(sd), 3000, f)
+            b = oracle.sample_partition(int(sd), 3000, f)
+            assert a == b.tolist(), (f, len(a), len(b))
+    # the filter keeps about f of the rows, gap sampling too
+    for f in (0.1, 0.7):
+        m = sum(len(oracle.sample_partition(int(sd), 20000, f)) for sd in oracle.partition_seeds(46, 5))
+        assert abs(m / 100000 - f) < 0.01
