@@ -327,9 +327,8 @@ __device__ __forceinline__ void ring_loader(const ChainLaunch& L, const ChainDes
     // sampled epoch: sample t is row rows[t], read with scalar loads (constant address space)
     const int32_t __attribute__((address_space(4)))* RIDX =
         (const int32_t __attribute__((address_space(4)))*)dsc.rows;
-    auto issue_row = [&](int64_t t) __attribute__((always_inline)) {
+    auto issue_row = [&](int64_t r) __attribute__((always_inline)) {   // r: partition row
         char* dst = ring + slot * ROW_BYTES;
-        const int64_t r = RIDX ? (int64_t)RIDX[t] : t;
         const V* row = reinterpret_cast<const V*>(X + r * ld);
         // every lane issues (past the row end it re-reads the row's first vector, bytes the
         // consumers ignore): each row is exactly NV vmcnt entries, which the counted waits need
@@ -388,10 +387,15 @@ __device__ __forceinline__ void ring_loader(const ChainLaunch& L, const ChainDes
             mslot = (mslot + 1 == MB) ? 0 : mslot + 1;
         }
         if (te - t == PUB) {
+            if (RIDX) {
 #pragma unroll
-            for (int k = 0; k < PUB; ++k) issue_row(t + k);
+                for (int k = 0; k < PUB; ++k) issue_row(RIDX[t + k]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < PUB; ++k) issue_row(t + k);
+            }
         } else {
-            for (int64_t u = t; u < te; ++u) issue_row(u);
+            for (int64_t u = t; u < te; ++u) issue_row(RIDX ? (int64_t)RIDX[u] : u);
         }
         if (te > D) {
             // all but the youngest D rows' instructions are done: rows < te - D have landed

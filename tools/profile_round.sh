@@ -8,7 +8,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
-ARGS=${BENCH_ARGS:-"--no-cpu-baseline --steps 3 --warmup 1"}
+ARGS=${BENCH_ARGS:-"--no-cpu-baseline"}   # the bench defaults (5 timed steps, 2 warmup)
 mkdir -p $OUT
 step() { echo "== $1"; shift; "$@"; rc=$?; echo "rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
 step trace timeout -k 10 240 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- python3 bench.py $ARGS
