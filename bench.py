@@ -27,7 +27,10 @@ WORKLOADS = {
            "Least-squares linear regression, dense 10M x 512 fp32, 256 chains on 1 MI355X"),
     "c3": ("logistic", 12_500_000, 1024, 256, 1.0, "f32",
            "Logistic regression, dense 100M x 1024 (per-GPU shard: 12.5M rows, 256 of 2048 chains)"),
+    "c4": ("hinge", 20_000_000, 47_236, 256, 1.0, "f32",
+           "Hinge-loss linear SVM, sparse CSR rcv1-like (47,236 features, 94 nnz/row = 0.2%)"),
 }
+CSR_NNZ = 94  # c4: nonzeros per row (rcv1's mean)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
@@ -52,6 +55,8 @@ def pmc_traffic(workload, grad, variant, storage):
 def kernel_name(variant):
     if 300 <= variant < 400:
         return f"chain_block (NV={variant - 300}: blocked fp32 chain, 8-row Gram blocks)"
+    if 400 <= variant < 500:
+        return "chain_sparse (fp32 CSR chain, weights L2/MALL-resident, one gather round trip per sample)"
     if 100 <= variant < 200:
         return f"chain_dense (NV={variant - 100}: per-sample chain)"
     return f"chain_general (variant {variant})"
@@ -93,7 +98,36 @@ def make_shard(torch, dev, n, d, P, grad, dtype, seed):
     return X, y, offs
 
 
-def cpu_baseline(grad, d, P, step, budget_s, seed=7):
+def make_csr_shard(torch, dev, n, d, P, grad, dtype, seed, nnz=CSR_NNZ):
+    """Synthetic rcv1-like CSR rows in HBM: nnz distinct sorted indices per
+    row (one uniform draw in each of nnz equal column buckets), values U(0,1) L2-normalised per
+    row, labels y = 1{w*.x + Logistic(0,1) > 0} from a planted w* ~ N(0,1)."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    tdt = torch.float32 if dtype == "f32" else torch.float64
+    width = d // nnz
+    col = torch.empty((n, nnz), dtype=torch.int32, device=dev)
+    val = torch.empty((n, nnz), dtype=tdt, device=dev)
+    y = torch.empty(n, dtype=torch.float64, device=dev)
+    w_star = torch.randn(d, generator=g, device=dev, dtype=torch.float64)
+    base = (torch.arange(nnz, device=dev, dtype=torch.int64) * width)[None, :]
+    chunk = 1 << 18
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        c = base + torch.randint(0, width, (b - a, nnz), generator=g, device=dev)
+        v = torch.rand((b - a, nnz), generator=g, device=dev, dtype=torch.float64)
+        v = v / v.norm(dim=1, keepdim=True)
+        col[a:b] = c.to(torch.int32)
+        val[a:b] = v.to(tdt)
+        z = (val[a:b].to(torch.float64) * w_star[c]).sum(1)
+        u = torch.rand(b - a, generator=g, device=dev, dtype=torch.float64).clamp_(1e-12, 1 - 1e-12)
+        y[a:b] = ((z + torch.log(u) - torch.log1p(-u)) > 0).to(torch.float64)
+    row_ptr = torch.arange(n + 1, dtype=torch.int64, device=dev) * nnz
+    offs = [i * n // P for i in range(P)] + [n]
+    return row_ptr, col.reshape(-1), val.reshape(-1), y, offs
+
+
+def cpu_baseline(grad, d, P, step, budget_s, seed=7, csr_nnz=0):
     """Time the CPU restatement of the reference (oracle/, one thread per partition, all host
     cores) on a bounded sample of the same workload: the first m rows of every partition."""
     import numpy as np
@@ -109,14 +143,22 @@ def cpu_baseline(grad, d, P, step, budget_s, seed=7):
         z = X @ w
         y = z + 0.1 * rng.standard_normal(P * m) if grad == "least_squares" else \
             ((z + rng.logistic(size=P * m)) > 0).astype(float)
-        return X, y
+        return O.Matrix(y, X)
+
+    def sample_csr(m):
+        width = d // csr_nnz
+        col = (np.arange(csr_nnz) * width)[None, :] + rng.integers(0, width, (P * m, csr_nnz))
+        val = rng.uniform(size=(P * m, csr_nnz))
+        val = (val / np.linalg.norm(val, axis=1, keepdims=True)).astype(np.float32).astype(np.float64)
+        y = (rng.uniform(size=P * m) > 0.5).astype(float)
+        rp = np.arange(P * m + 1, dtype=np.int64) * csr_nnz
+        return O.Matrix(y, row_ptr=rp, col=col.reshape(-1).astype(np.int32), val=val.reshape(-1), d=d)
 
     # A sample of m rows per partition (host memory bounded), re-run as successive epochs until
     # the time budget is spent: per-epoch CPU cost does not depend on which rows are used.
-    m = 1024 if d <= 1024 else 256
-    X, y = sample(m)
+    m = 1024 if (csr_nnz or d <= 1024) else 256
+    mat = sample_csr(m) if csr_nnz else sample(m)
     offs = [p * m for p in range(P + 1)]
-    mat = O.Matrix(y, X)
     w = np.zeros(d)
     total, epochs = 0, 0
     t0 = time.perf_counter()
@@ -131,7 +173,8 @@ def cpu_baseline(grad, d, P, step, budget_s, seed=7):
             break
     return {"value": total / dt, "unit": "samples/s", "cores": cores, "kind": "port",
             "sample": f"oracle/psgd_oracle.c (fp64 CPU restatement of ParallelizedSGD.scala:243-270 "
-                      f"incl. per-sample isConverged), {P} partitions x {m} rows, d={d}, "
+                      f"incl. per-sample isConverged), {P} partitions x {m} "
+                      f"{'CSR (%d nnz) ' % csr_nnz if csr_nnz else ''}rows, d={d}, "
                       f"{epochs} epochs, {cores} threads, {dt:.1f} s"}
 
 
@@ -154,18 +197,27 @@ def main():
     grad, n, d, P, step, sdt, cfg_name = WORKLOADS[args.workload]
     if args.rows:
         n = args.rows
-    X, y, offs = make_shard(torch, dev, n, d, P, grad, sdt, 1000 + rank)
-    torch.cuda.synchronize()
-    parts = [pkg.DevicePartition(y[a:b], X[a:b], d) for a, b in zip(offs[:-1], offs[1:])]
+    csr = args.workload == "c4"
+    if csr:
+        rp, col, val, y, offs = make_csr_shard(torch, dev, n, d, P, grad, sdt, 1000 + rank)
+        torch.cuda.synchronize()
+        parts = [pkg.DeviceCsrPartition(y[a:b], rp[a:b + 1], col, val, d) for a, b in zip(offs[:-1], offs[1:])]
+        empty = lambda: pkg.DeviceCsrPartition(y[:0], rp[:1], col, val, d)
+    else:
+        X, y, offs = make_shard(torch, dev, n, d, P, grad, sdt, 1000 + rank)
+        torch.cuda.synchronize()
+        parts = [pkg.DevicePartition(y[a:b], X[a:b], d) for a, b in zip(offs[:-1], offs[1:])]
+        empty = lambda: pkg.DevicePartition(y[:0], X[:0], d)
     # global partition list: this rank's block is [rank*P, (rank+1)*P)
     all_parts = [None] * (P * world)
     all_parts[rank * P:(rank + 1) * P] = parts
     for i in range(len(all_parts)):
         if all_parts[i] is None:
-            all_parts[i] = pkg.DevicePartition(y[:0], X[:0], d)  # placeholders for other ranks
+            all_parts[i] = empty()  # placeholders for other ranks
     data = pkg.PartitionedData(all_parts)
     engine = pkg.HipEngine(data, rank, world, device=local)
-    gcls = pkg.LeastSquaresGradient() if grad == "least_squares" else pkg.LogisticGradient()
+    gcls = {"least_squares": pkg.LeastSquaresGradient, "logistic": pkg.LogisticGradient,
+            "hinge": pkg.HingeGradient}[grad]()
     params = pkg.make_params(gcls, pkg.SimpleSGDUpdater(), step, 0.0, 1.0, 0.0, args.compute)
     import numpy as np
     w = engine.weights(np.zeros(d))
@@ -216,7 +268,10 @@ def main():
     avg_epoch_s = sum(epoch_ms) / len(epoch_ms) / 1e3
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
     es = 4 if sdt == "f32" else 8
-    bytes_per_sample = (d + 1) * es  # row + label (weights are on chip)
+    if csr:  # values + int32 columns + int64 row pointer + f64 label (weights: L2/MALL-resident)
+        bytes_per_sample = CSR_NNZ * (es + 4) + 8 + 8
+    else:
+        bytes_per_sample = (d + 1) * es  # row + label (weights are on chip)
     local_samples = n
     # one chain-kernel launch processes every row of this GPU's partitions
     achieved = local_samples * bytes_per_sample / avg_kernel_s / 1e9
@@ -241,7 +296,8 @@ def main():
                      "timing": "HIP events recorded around each chain-kernel launch on its stream"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(grad, d, P, step, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(grad, d, P, step, args.cpu_seconds,
+                                           csr_nnz=CSR_NNZ if csr else 0)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -105,6 +105,14 @@ int32_t psgd_register_dense_device(psgd_ctx* ctx, int64_t part, int64_t n_rows, 
                                    int64_t ld, const double* d_labels, const void* d_x,
                                    int32_t dtype);
 
+/* Zero-copy registration of a CSR partition already resident on the context's device:
+ * d_row_ptr[n_rows+1] int64 absolute offsets into d_col/d_val (non-decreasing), d_col[] int32
+ * strictly increasing within a row and < d, d_val[] of `dtype`, d_labels[n_rows]. The contents
+ * are not validated (they are on the device); the caller keeps the buffers alive. */
+int32_t psgd_register_csr_device(psgd_ctx* ctx, int64_t part, int64_t n_rows, int32_t d,
+                                 const double* d_labels, const int64_t* d_row_ptr,
+                                 const int32_t* d_col, const void* d_val, int32_t dtype);
+
 int32_t psgd_clear_partitions(psgd_ctx* ctx);
 int32_t psgd_num_partitions(psgd_ctx* ctx, int64_t* n_parts, int64_t* n_rows_total);
 

@@ -10,7 +10,8 @@ registers it as `spark_parallelized_sgd_amd`).
 """
 from ._native import (DeviceError, IllegalArgumentException, UnsupportedOperationException,
                       build)
-from .data import CsrPartition, DensePartition, DevicePartition, PartitionedData, shard_range
+from .data import (CsrPartition, DensePartition, DeviceCsrPartition, DevicePartition, PartitionedData,
+                   shard_range)
 from .gradient import Gradient, HingeGradient, LeastSquaresGradient, LogisticGradient
 from .optimization import (HipEngine, ParallelizedSGD, ShardedEngine, make_params,
                            runParallelizedSGD)
@@ -22,6 +23,7 @@ __all__ = [
     "Gradient", "LogisticGradient", "LeastSquaresGradient", "HingeGradient",
     "SGDUpdater", "SimpleSGDUpdater", "SquaredL2SGDUpdater", "L1SGDUpdater",
     "AdaGradSGDUpdater", "AdamSGDUpdater",
-    "PartitionedData", "DensePartition", "CsrPartition", "DevicePartition", "shard_range",
+    "PartitionedData", "DensePartition", "CsrPartition", "DevicePartition", "DeviceCsrPartition",
+    "shard_range",
     "IllegalArgumentException", "UnsupportedOperationException", "DeviceError", "build",
 ]

@@ -20,7 +20,7 @@ F64, F32 = 0, 1
 # Symbols include/psgd.h declares (checked by tests/test_capi_symbols.py).
 EXPORTED = (
     "psgd_abi_version", "psgd_last_error", "psgd_ctx_create", "psgd_ctx_destroy",
-    "psgd_register_dense", "psgd_register_csr", "psgd_register_dense_device",
+    "psgd_register_dense", "psgd_register_csr", "psgd_register_dense_device", "psgd_register_csr_device",
     "psgd_clear_partitions", "psgd_num_partitions", "psgd_run_epoch", "psgd_run_epoch_device",
     "psgd_fold_partials_device", "psgd_convergence_terms_device", "psgd_initial_regval",
     "psgd_ctx_last_kernel", "psgd_ctx_last_chain_ms",
@@ -83,6 +83,7 @@ def lib():
             "psgd_register_dense": ([vp, C.c_int64, C.c_int64, C.c_int32, vp, vp, C.c_int32], C.c_int32),
             "psgd_register_csr": ([vp, C.c_int64, C.c_int64, C.c_int32, vp, vp, vp, vp, C.c_int32], C.c_int32),
             "psgd_register_dense_device": ([vp, C.c_int64, C.c_int64, C.c_int32, C.c_int64, vp, vp, C.c_int32], C.c_int32),
+            "psgd_register_csr_device": ([vp, C.c_int64, C.c_int64, C.c_int32, vp, vp, vp, vp, C.c_int32], C.c_int32),
             "psgd_clear_partitions": ([vp], C.c_int32),
             "psgd_num_partitions": ([vp, i64p, i64p], C.c_int32),
             "psgd_run_epoch": ([vp, P, vp, vp, dp, dp, i64p, vp], C.c_int32),
@@ -160,6 +161,10 @@ class Context:
     def register_dense_device(self, part, n_rows, d, ld, labels_ptr, x_ptr, dtype):
         check(self._L.psgd_register_dense_device(self.handle, part, n_rows, d, ld, labels_ptr,
                                                  x_ptr, dtype))
+
+    def register_csr_device(self, part, n_rows, d, labels_ptr, row_ptr_ptr, col_ptr, val_ptr, dtype):
+        check(self._L.psgd_register_csr_device(self.handle, part, n_rows, d, labels_ptr, row_ptr_ptr,
+                                               col_ptr, val_ptr, dtype))
 
     def clear(self):
         check(self._L.psgd_clear_partitions(self.handle))

@@ -54,6 +54,7 @@ struct Part {
     int64_t* row_ptr = nullptr;
     int32_t* col = nullptr;
     int64_t ld = 0;
+    int64_t max_nnz = 0;      // CSR: the longest row
 };
 
 // Device buffer that only grows.
@@ -135,7 +136,7 @@ struct psgd_ctx {
     std::mutex mu;
     std::map<int64_t, Part> parts;
     bool descs_dirty = true;
-    DevBuf descs, w_in, w_out, state, rv, loss, cnt_d, cnt, steps, partial, tmp, watchdog, zbuf;
+    DevBuf descs, w_in, w_out, state, rv, loss, cnt_d, cnt, steps, partial, tmp, watchdog, zbuf, wf32, stamps;
     DevBuf sdescs, srows, sys, xstate;   // sampled epochs (miniBatchFraction < 1)
     double steps_value = NAN;
     int64_t steps_n = 0;
@@ -309,7 +310,7 @@ int32_t psgd_ctx_destroy(psgd_ctx* ctx) {
         hipStreamSynchronize(ctx->stream);
         for (auto& kv : ctx->parts) free_part(kv.second);
         for (DevBuf* b : {&ctx->descs, &ctx->w_in, &ctx->w_out, &ctx->state, &ctx->rv, &ctx->loss,
-                          &ctx->cnt_d, &ctx->cnt, &ctx->steps, &ctx->partial, &ctx->tmp, &ctx->zbuf,
+                          &ctx->cnt_d, &ctx->cnt, &ctx->steps, &ctx->partial, &ctx->tmp, &ctx->zbuf, &ctx->wf32, &ctx->stamps,
                           &ctx->sdescs, &ctx->srows, &ctx->sys, &ctx->xstate,
                           &ctx->watchdog})
             b->release();
@@ -389,6 +390,41 @@ int32_t psgd_register_dense_device(psgd_ctx* ctx, int64_t part, int64_t n_rows, 
     return PSGD_OK;
 }
 
+int32_t psgd_register_csr_device(psgd_ctx* ctx, int64_t part, int64_t n_rows, int32_t d,
+                                 const double* d_labels, const int64_t* d_row_ptr,
+                                 const int32_t* d_col, const void* d_val, int32_t dtype) {
+    if (!ctx) return fail(PSGD_EINVAL, "ctx is null");
+    if (part < 0) return fail(PSGD_EINVAL, "partition index must be non-negative");
+    if (n_rows < 0 || d <= 0) return fail(PSGD_EINVAL, "n_rows must be >= 0 and d > 0");
+    if (dtype != PSGD_F64 && dtype != PSGD_F32) return fail(PSGD_EINVAL, "unknown dtype");
+    if (n_rows > 0 && (!d_labels || !d_row_ptr || !d_col || !d_val))
+        return fail(PSGD_EINVAL, "labels/row_ptr/col/val are null");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    int32_t rc = check_compat(ctx, d, dtype, psgd::kCsr);
+    if (rc) return rc;
+    Part p;
+    p.n_rows = n_rows;
+    p.d = d;
+    p.dtype = dtype;
+    p.layout = psgd::kCsr;
+    p.owned = false;
+    p.x = const_cast<void*>(d_val);
+    p.y = const_cast<double*>(d_labels);
+    p.row_ptr = const_cast<int64_t*>(d_row_ptr);
+    p.col = const_cast<int32_t*>(d_col);
+    p.ld = 0;
+    {
+        DeviceGuard g(ctx->device);
+        int e = psgd::csr_max_nnz(d_row_ptr, n_rows, &p.max_nnz, ctx->stream);
+        if (e) return fail(PSGD_EDEVICE, "row length scan failed");
+    }
+    auto it = ctx->parts.find(part);
+    if (it != ctx->parts.end()) free_part(it->second);
+    ctx->parts[part] = p;
+    ctx->descs_dirty = true;
+    return PSGD_OK;
+}
+
 int32_t psgd_register_csr(psgd_ctx* ctx, int64_t part, int64_t n_rows, int32_t d,
                           const double* labels, const int64_t* row_ptr, const int32_t* col,
                           const void* val, int32_t dtype) {
@@ -428,6 +464,8 @@ int32_t psgd_register_csr(psgd_ctx* ctx, int64_t part, int64_t n_rows, int32_t d
     p.dtype = dtype;
     p.layout = psgd::kCsr;
     p.owned = true;
+    for (int64_t r = 0; r < n_rows; ++r)
+        p.max_nnz = std::max<int64_t>(p.max_nnz, rp[(size_t)r + 1] - rp[(size_t)r]);
     if (n_rows > 0) {
         HIP_TRY(hipMalloc((void**)&p.row_ptr, rp.size() * sizeof(int64_t)));
         HIP_TRY(hipMalloc((void**)&p.y, (size_t)n_rows * sizeof(double)));
@@ -493,9 +531,10 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
     const int state_vectors = !need_state ? 0 : layout == psgd::kCsr ? 3 : 2;
     rc = prepare(ctx, d, state_vectors, st);
     if (rc) return rc;
-    int64_t n_max = 0, max_ld = 0, min_ld = INT64_MAX;
+    int64_t n_max = 0, max_ld = 0, min_ld = INT64_MAX, max_nnz = 0;
     for (auto& kv : ctx->parts) {
         n_max = std::max(n_max, kv.second.n_rows);
+        max_nnz = std::max(max_nnz, kv.second.max_nnz);
         if (kv.second.n_rows > 0) {
             max_ld = std::max(max_ld, kv.second.ld);
             min_ld = std::min(min_ld, kv.second.ld);
@@ -548,8 +587,26 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
     L.steps = ctx->steps.as<double>();
     L.watchdog = ctx->watchdog.as<int>();
     L.stamps = nullptr;
+    static const bool want_stamps = [] {
+        const char* e = getenv("PSGD_STAMPS");
+        return e && *e && *e != '0';
+    }();
+    if (want_stamps && layout == psgd::kCsr) {
+        HIP_TRY(ctx->stamps.ensure((size_t)P * 4 * sizeof(unsigned long long)));
+        HIP_TRY(hipMemsetAsync(ctx->stamps.p, 0, (size_t)P * 4 * sizeof(unsigned long long), st));
+        L.stamps = ctx->stamps.as<unsigned long long>();
+    }
     L.zbuf = nullptr;
     L.zstride = 0;
+    L.wf32 = nullptr;
+    L.wstride = 0;
+    if (layout == psgd::kCsr && params->compute_dtype == PSGD_F32) {
+        // fp32 working weights of the CSR kernel (one d-vector per chain, HBM/L2-resident, and
+        // 128 floats the kernel's masked-off lanes load from / store to)
+        L.wstride = (int64_t)d + 128;
+        HIP_TRY(ctx->wf32.ensure((size_t)P * (size_t)L.wstride * sizeof(float)));
+        L.wf32 = ctx->wf32.as<float>();
+    }
     if (params->gradient == PSGD_GRADIENT_LOGISTIC && params->compute_dtype == PSGD_F32 &&
         layout == psgd::kDense) {
         // per-row margins of the fp32 Logistic block kernel (its loss is summed after the chain)
@@ -585,9 +642,22 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         int e = psgd::launch_chains(L, kp, layout, first.dtype == PSGD_F32 ? 1 : 0,
                                     params->compute_dtype == PSGD_F32 ? 1 : 0, params->gradient,
                                     params->updater, conv, min_ld, max_ld,
-                                    lds_spread_bytes(ctx, (size_t)P), st, &ctx->last_variant);
+                                    lds_spread_bytes(ctx, (size_t)P), st, &ctx->last_variant, max_nnz);
         HIP_TRY(hipEventRecord(ctx->ev_end, st));
         ctx->ev_recorded = (e == 0);
+        if (L.stamps) {   // PSGD_STAMPS=1: per-chain cycle counters of the CSR fp32 kernel (stderr)
+            std::vector<unsigned long long> h((size_t)P * 4);
+            HIP_TRY(hipMemcpyAsync(h.data(), L.stamps, h.size() * 8, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            std::vector<double> v[4];
+            for (int p = 0; p < P; ++p)
+                for (int k = 0; k < 4; ++k) v[k].push_back((double)h[(size_t)p * 4 + k] / std::max<int64_t>(n_max, 1));
+            const char* names[4] = {"chain.total", "chain.wait_ready", "helper.total", "helper.wait_done"};
+            for (int k = 0; k < 4; ++k) {
+                std::sort(v[k].begin(), v[k].end());
+                fprintf(stderr, "psgd stamps %-18s cycles/row median %8.1f\n", names[k], v[k][v[k].size() / 2]);
+            }
+        }
         if (e == -2) return fail(PSGD_EUNSUPPORTED, "this gradient/updater/layout combination is not built");
         if (e) return fail(PSGD_EDEVICE, std::string("chain kernel launch failed: ") +
                                              hipGetErrorString((hipError_t)e));

@@ -45,6 +45,8 @@ struct ChainLaunch {
     unsigned long long* stamps;  // per-wave cycle counters, diagnostic builds only (PSGD_STAMPS)
     float* zbuf;             // [n_chains * zstride] per-row margins (fp32 Logistic block kernel)
     int64_t zstride;
+    float* wf32;             // [n_chains * wstride] fp32 working weights (CSR fp32 kernel)
+    int64_t wstride;
 };
 
 // Diagnostic builds (-DPSGD_STAMPS, tools/chain_bench.hip) count s_memtime cycles per wave.
@@ -58,7 +60,7 @@ struct ChainLaunch {
 // storage: 0 = f64, 1 = f32; compute: 0 = f64, 1 = f32.
 int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int storage, int compute,
                   int gradient, int updater, bool check_conv, int64_t min_ld, int64_t max_ld,
-                  int lds_spread, hipStream_t stream, int* kernel_variant);
+                  int lds_spread, hipStream_t stream, int* kernel_variant, int64_t max_nnz = 0);
 // The blocked fp32 kernel (psgd_block.hip): dense rows, Simple/SquaredL2, no per-sample
 // convergence test. launch_block_chains returns -3 when it does not apply.
 bool block_path_applies(int layout, int compute, int updater, bool check_conv, int storage,
@@ -71,6 +73,12 @@ int launch_fold(const double* w, int64_t w_stride, const double* rv, const doubl
                 const int* watchdog, hipStream_t stream);
 int launch_sq_terms(const double* a, const double* b, int d, double* out2, hipStream_t stream);
 int launch_steps(double step, int64_t n, double* steps, hipStream_t stream);
+// The fp32 CSR kernel (psgd_sparse.hip): weights as fp32 vectors in HBM (L.wf32).
+bool sparse_path_applies(int layout, int compute, int updater, bool check_conv);
+int launch_sparse_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
+                         int updater, int64_t max_nnz, hipStream_t stream, int* kernel_variant);
+// Longest row of a device-resident CSR partition (synchronises `st`).
+int csr_max_nnz(const int64_t* d_row_ptr, int64_t n, int64_t* out, hipStream_t st);
 // RDD.sample(false, fraction, seed) per partition (PSGD.scala:242): from the registered
 // descriptors `base`, the epoch's descriptors `out` (rows/y/n_rows of the sampled subsequence;
 // rows and labels in `rows`/`ys`, `stride` entries per chain). xs_state[c] is the chain's

@@ -690,7 +690,7 @@ static int dispatch_grad(const ChainLaunch& L, const KParams& kp, int layout, in
 
 int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int storage, int compute,
                   int gradient, int updater, bool check_conv, int64_t min_ld, int64_t max_ld,
-                  int lds_spread, hipStream_t stream, int* kernel_variant) {
+                  int lds_spread, hipStream_t stream, int* kernel_variant, int64_t max_nnz) {
     if (kp.n_chains <= 0) return 0;
     // PSGD_PER_SAMPLE=1 keeps fp32 mode on the per-sample kernel (A/B measurements)
     static const bool per_sample = [] {
@@ -700,6 +700,8 @@ int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int stora
     if (!per_sample && block_path_applies(layout, compute, updater, check_conv, storage, max_ld))
         return launch_block_chains(L, kp, storage, gradient, updater, min_ld, max_ld, lds_spread,
                                    stream, kernel_variant);
+    if (!per_sample && sparse_path_applies(layout, compute, updater, check_conv))
+        return launch_sparse_chains(L, kp, storage, gradient, updater, max_nnz, stream, kernel_variant);
     const size_t lds = (size_t)(lds_spread > 0 ? lds_spread : 0);
     if (storage == 1)
         return dispatch_grad<float>(L, kp, layout, compute, gradient, updater, check_conv, min_ld,

@@ -1,0 +1,648 @@
+// psgd_sparse.hip -- the fp32 throughput-mode chain for CSR rows (gfx950).
+//
+// Reference: ParallelizedSGD.scala:243-270 (the chain), [ext] MLlib 1.6.1 Gradient.scala
+// (Logistic / LeastSquares / Hinge on SparseVector rows: the gradient is mult * x, non-zero only
+// at the row's indices), SGDUpdater.scala:86-98 (Simple) and :163-181 (SquaredL2).
+//
+// Wide sparse models (rcv1: 47,236 features; 2^22 in BASELINE config 5) do not fit a CU's LDS,
+// so each chain keeps its weights as an fp32 vector in HBM (P x d floats: 48 MB at rcv1 shape,
+// L2/MALL-resident) and one wave walks the partition:
+//   * lane l owns the row's entries l, l+64, ... (two per lane for rows of <= 128 non-zeros);
+//   * the weights at those indices are gathered with L1-bypassing (sc1) loads, which the same
+//     wave's earlier plain stores to the same addresses precede in L2: consecutive rows that
+//     share a feature see the updated value;
+//   * the next row's (col, val), label and step, and the row pointers of the row after it, are
+//     loaded while the current row's gather is in flight, so a sample costs one gather round
+//     trip plus the wave reduction;
+//   * the update touches only the row's indices (w_j += c x_j); Hinge rows inside the margin
+//     (c = 0) store nothing.
+// SquaredL2 scales every coordinate by a_t = 1 - s_t*lambda each sample (UPD.scala:169): the
+// chain keeps w = alpha * v (alpha in f64), so the scale is one multiply of alpha and an update
+// adds c x_j / alpha to v_j (the alpha-scaled lazy form). regVal needs ||w|| after
+// the chain's last sample only (PSGD.scala:257): 0.5 * lambda * alpha^2 * ||v||^2.
+// No MFMA, no LDS: the work per sample is a 94-long gather-dot and scatter.
+#include "psgd_device.h"
+
+#include <stdlib.h>
+
+namespace psgd {
+
+template <int GRAD>
+__device__ __forceinline__ float sparse_coef(float z, float y, float s, float& loss) {
+    if constexpr (GRAD == G_LEAST_SQUARES) {
+        const float diff = z - y;
+        loss = diff * diff;                      // halved once at the end
+        return -s * diff;
+    } else if constexpr (GRAD == G_LOGISTIC) {
+        const float margin = -z;
+        const float e = __expf(margin);
+        const float sig = __builtin_amdgcn_rcpf(1.0f + e);
+        const float ax = __builtin_fabsf(margin);
+        const float l = __logf(1.0f + __expf(-ax)) + (margin > 0.0f ? margin : 0.0f);
+        loss = y > 0.0f ? l : l - margin;
+        return -s * (sig - y);
+    } else {
+        const float ls = 2.0f * y - 1.0f;
+        const float lz = ls * z;
+        const bool on = 1.0f > lz;
+        loss = on ? 1.0f - lz : 0.0f;
+        return on ? s * ls : 0.0f;
+    }
+}
+
+template <typename S, int GRAD, int UPD>
+__global__ __launch_bounds__(64) void chain_sparse(ChainLaunch L, KParams kp) {
+    constexpr bool L2 = UPD == U_SQUARED_L2;
+    const int lane = threadIdx.x;
+    const int chain = blockIdx.x;
+    const ChainDesc dsc = L.descs[chain];
+    const int d = kp.d;
+    const int64_t n = dsc.n_rows;
+    const gptr<S> X = as_global(reinterpret_cast<const S*>(dsc.x));
+    const gptr<int32_t> COL = as_global(dsc.col);
+    const gptr<int64_t> RP = as_global(dsc.row_ptr);
+    const gptr<double> Y = as_global(dsc.y);
+    const gptr<double> STEPS = as_global(L.steps);
+    const gptr<int32_t> RIDX = dsc.rows ? as_global(dsc.rows) : nullptr;   // sampled epoch
+    float* V = L.wf32 + (int64_t)chain * L.wstride;
+    const gmut<float> VW = as_global_mut(V);
+
+    for (int i = lane; i < d; i += 64) VW[i] = float(as_global(L.w_in)[i]);
+    // the chain's gathers below are loads of these addresses from the same wave
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    double alpha = 1.0;      // SquaredL2: w = alpha * v
+    double loss_sum = 0.0;
+    float loss_blk = 0.0f;
+    int64_t count = 0;
+
+    // Software pipeline: row t+2's entry range is loaded during sample t, row t+1's entries,
+    // label and step during sample t (their range is known by then), so the only round trip a
+    // sample waits for is its own gather.
+    auto row_of = [&](int64_t t) __attribute__((always_inline)) -> int64_t {
+        return RIDX ? (int64_t)RIDX[t] : t;
+    };
+    auto range_of = [&](int64_t t, int64_t& b, int64_t& e) __attribute__((always_inline)) {
+        if (t < n) {
+            const int64_t r = row_of(t);
+            b = RP[r];
+            e = RP[r + 1];
+        } else {
+            b = e = 0;
+        }
+    };
+    auto entries_of = [&](int64_t t, int64_t b, int64_t e, double& yy, double& ss, int32_t& ca,
+                          int32_t& cb, float& xa, float& xb) __attribute__((always_inline)) {
+        yy = t < n ? Y[t] : 0.0;
+        ss = t < n ? STEPS[t] : 0.0;
+        const int64_t ka = b + lane, kc = b + 64 + lane;
+        ca = ka < e ? COL[ka] : 0;
+        xa = ka < e ? float(X[ka]) : 0.0f;
+        cb = kc < e ? COL[kc] : 0;
+        xb = kc < e ? float(X[kc]) : 0.0f;
+    };
+    int64_t kb = 0, ke = 0, kb1 = 0, ke1 = 0;     // ranges of rows t and t+1
+    double y = 0.0, s = 0.0;
+    int32_t c0 = 0, c1 = 0;
+    float x0 = 0.0f, x1 = 0.0f;
+    range_of(0, kb, ke);
+    range_of(1, kb1, ke1);
+    entries_of(0, kb, ke, y, s, c0, c1, x0, x1);
+
+    for (int64_t t = 0; t < n; ++t) {
+        const int64_t nnz = ke - kb;
+        const bool a0 = lane < nnz, a1 = lane + 64 < nnz;
+        // gather (sc1: served by L2, after this wave's earlier stores to the same lines)
+        float w0 = a0 ? __hip_atomic_load(&V[c0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0f;
+        float w1 = a1 ? __hip_atomic_load(&V[c1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0f;
+        // under the gather: row t+1's entries (its range is known), row t+2's range
+        double ny = 0.0, ns = 0.0;
+        int32_t n0 = 0, n1 = 0;
+        float nx0 = 0.0f, nx1 = 0.0f;
+        entries_of(t + 1, kb1, ke1, ny, ns, n0, n1, nx0, nx1);
+        int64_t kb2, ke2;
+        range_of(t + 2, kb2, ke2);
+
+        float acc = x0 * w0;
+        acc = __builtin_fmaf(x1, w1, acc);
+        // entries past the first 128 (rows wider than two per lane)
+        for (int64_t k = kb + 128 + lane; k < ke; k += 64)
+            acc = __builtin_fmaf(float(X[k]), __hip_atomic_load(&V[COL[k]], __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_AGENT), acc);
+        float z = wave_sum_uniform(acc);
+        const float sf = float(s);
+        if constexpr (L2) {
+            // w <- a w + c x: alpha absorbs a; the dot was taken against w = alpha v
+            z = float(alpha * double(z));
+            alpha *= 1.0 - s * kp.reg;
+        }
+        float loss;
+        const float c = sparse_coef<GRAD>(z, float(y), sf, loss);
+        loss_blk += loss;
+        if ((t & 31) == 31) { loss_sum += double(loss_blk); loss_blk = 0.0f; }
+        count += 1;
+        if (c != 0.0f) {
+            const float cv = L2 ? float(double(c) / alpha) : c;
+            if (a0) VW[c0] = __builtin_fmaf(cv, x0, w0);
+            if (a1) VW[c1] = __builtin_fmaf(cv, x1, w1);
+            for (int64_t k = kb + 128 + lane; k < ke; k += 64) {
+                const int32_t j = COL[k];
+                VW[j] = __builtin_fmaf(cv, float(X[k]), __hip_atomic_load(&V[j], __ATOMIC_RELAXED,
+                                                                          __HIP_MEMORY_SCOPE_AGENT));
+            }
+        }
+        kb = kb1; ke = ke1; kb1 = kb2; ke1 = ke2;
+        y = ny; s = ns; c0 = n0; c1 = n1; x0 = nx0; x1 = nx1;
+    }
+    loss_sum += double(loss_blk);
+    if constexpr (GRAD == G_LEAST_SQUARES) loss_sum = loss_sum / 2.0;
+
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // the chain's weights (w = alpha v) and regVal of its last update (PSGD.scala:257)
+    double nsq = 0.0;
+    double* wo = L.w_out + (int64_t)chain * d;
+    for (int i = lane; i < d; i += 64) {
+        const double wv = alpha * double(__hip_atomic_load(&V[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        wo[i] = wv;
+        if constexpr (L2) nsq += wv * wv;
+    }
+    double rv = 0.0;
+    if constexpr (L2) {
+        nsq = wave_sum(nsq);
+        if (count > 0) {
+            const double nrm = sqrt(nsq);
+            rv = 0.5 * kp.reg * nrm * nrm;
+        }
+    }
+    if (lane == 0) {
+        L.rv[chain] = rv;
+        L.loss[chain] = loss_sum;
+        L.cnt[chain] = count;
+        L.cnt_d[chain] = double(count);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// chain_sparse_spec: the same chain with the gathers issued SK samples ahead (rows of <= 128
+// non-zeros, d small enough for a per-feature tag table in LDS, 47,236 at rcv1 shape).
+//
+// A gather for row u issued during sample u-SK does not see the stores of rows u-SK .. u-1
+// (issued after it). A helper wave finds, for every entry of row u, the latest of those rows
+// that has the same feature: it keeps tagpos[j] = (row & 255) << 8 | entry of the last row that
+// touched feature j; an entry from outside the window is ignored, and a row's tags are cleared
+// before its LDS slot is reused (so an 8-bit row tag never aliases). The chain wave replaces such a gathered value by
+// that row's new value (kept in LDS) -- exactly the value the reference's sequential update
+// would read. Waves:
+//   wave 0 (chain)  per sample t: waits for row t's gather (issued SK samples earlier; a fixed
+//                   count of VMEM instructions per sample makes it s_waitcnt vmcnt(4 SK - 2)),
+//                   corrects it, dot + wave reduction + coefficient, issues the gather of row
+//                   t + SK, stores the row's new weights (to HBM and to its LDS slot);
+//   wave 1 (helper) loads the rows (64 row pointers / labels / steps per batch, entries of 8
+//                   rows per round trip) into an R-slot LDS ring with their correction entries.
+// ------------------------------------------------------------------------------------------
+constexpr int SK = 8;             // speculation depth (samples)
+constexpr int SR = 32;            // LDS row slots
+constexpr int SCAP = 128;         // entries per row (two per lane)
+// The chain at sample t needs row t + SK staged; the helper stages 8-row groups and may reuse
+// the slot of row u - SR once the chain is done with row u - SR + SK: it can always stage the
+// group holding row t + SK if SR >= 2 SK + 8.
+static_assert(SR >= 2 * SK + 8, "ring too small for the speculation depth");
+static_assert((SR & (SR - 1)) == 0, "slot index by mask");
+
+struct SpecHeader {
+    unsigned ready;   // rows staged by the helper
+    unsigned done;    // rows finished by the chain
+    unsigned stop;
+    unsigned pad;
+};
+struct SpecSlot {
+    int32_t col[SCAP];
+    float val[SCAP];
+    int16_t prev[SCAP];    // -1, or (row delta 1..SK) << 8 | entry of the latest earlier row
+    float nv[SCAP];        // the row's new weights (chain)
+    int32_t nnz;
+    int32_t pad;
+    double y, s;
+};
+
+// The chain's VMEM instructions are inline asm: their count per sample is what its vmcnt waits
+// rely on, so the compiler must neither merge nor drop any of them.
+__device__ __forceinline__ float gather_sc1(const float* p) {
+    float v;
+    asm volatile("global_load_dword %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ void store_f32(float* p, float v) {
+    asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");
+}
+
+template <typename S, int GRAD, int UPD>
+__global__ __launch_bounds__(128) void chain_sparse_spec(ChainLaunch L, KParams kp) {
+    constexpr bool L2 = UPD == U_SQUARED_L2;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    SpecHeader* hdr = reinterpret_cast<SpecHeader*>(smem);
+    SpecSlot* slots = reinterpret_cast<SpecSlot*>(smem + sizeof(SpecHeader));
+    uint16_t* tagpos = reinterpret_cast<uint16_t*>(smem + sizeof(SpecHeader) + SR * sizeof(SpecSlot));
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int chain = blockIdx.x;
+    const ChainDesc dsc = L.descs[chain];
+    const int d = kp.d;
+    const int64_t n = dsc.n_rows;
+    float* V = L.wf32 + (int64_t)chain * L.wstride;   // [d] weights + [128] dummy targets
+
+    for (int i = threadIdx.x; i < d; i += blockDim.x) tagpos[i] = 0xFFFF;
+    if (threadIdx.x == 0) { hdr->ready = 0; hdr->done = 0; hdr->stop = 0; }
+    if (wave == 0) {
+        for (int i = lane; i < d; i += 64) as_global_mut(V)[i] = float(as_global(L.w_in)[i]);
+    }
+    __syncthreads();
+
+    uint64_t st_wait = 0;                     // diagnostic: cycles spent waiting on the other wave
+    const uint64_t st_begin = __builtin_amdgcn_s_memtime();
+    auto spin = [&](const unsigned* flag, int64_t need, int code) __attribute__((always_inline)) -> bool {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        const uint64_t c0 = __builtin_amdgcn_s_memtime();
+        for (;;) {
+            // relaxed: the flags and the slots are LDS, which one wave reads and writes in order
+            if ((int64_t)__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= need) {
+                __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                st_wait += __builtin_amdgcn_s_memtime() - c0;
+                return true;
+            }
+            if (__hip_atomic_load(&hdr->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kWatchdogTicks) {
+                __hip_atomic_fetch_or(L.watchdog, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                return false;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    };
+
+    if (wave == 1) {
+        // ---------------- helper: stage rows with their correction entries ----------------
+        const gptr<S> X = as_global(reinterpret_cast<const S*>(dsc.x));
+        const gptr<int32_t> COL = as_global(dsc.col);
+        const gptr<int64_t> RP = as_global(dsc.row_ptr);
+        const gptr<double> Y = as_global(dsc.y);
+        const gptr<double> STEPS = as_global(L.steps);
+        const gptr<int32_t> RIDX = dsc.rows ? as_global(dsc.rows) : nullptr;
+        unsigned done = 0;
+        const void* dummy_i = (const void*)(V + d + lane);            // valid, never used
+        const void* dummy_s = (const void*)(V + d + 2 * lane);
+        // Software pipeline: the row ranges / labels / steps of the next 64-row batch and the
+        // entries of the next 8-row group are in flight while the current group is staged.
+        struct Batch { int64_t rb, re; double y, s; };
+        auto load_batch = [&](int64_t g) __attribute__((always_inline)) -> Batch {
+            Batch bt{0, 0, 0.0, 0.0};
+            const int64_t ti = g + lane;
+            if (ti < n) {
+                const int64_t r = RIDX ? (int64_t)RIDX[ti] : ti;
+                bt.rb = RP[r];
+                bt.re = RP[r + 1];
+                bt.y = Y[ti];
+                bt.s = STEPS[ti];
+            }
+            return bt;
+        };
+        struct Group { int32_t ca[8], cb[8]; float xa[8], xb[8]; int64_t b[8], e[8]; };
+        auto rl64 = [&](int64_t v, int i) __attribute__((always_inline)) -> int64_t {
+            return (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v & 0xffffffff), i) |
+                   ((int64_t)__builtin_amdgcn_readlane((int)(v >> 32), i) << 32);
+        };
+        // entries of rows g + i0 .. g + i0 + 7 of batch bt (rows past n: empty)
+        auto load_group = [&](const Batch& bt, int64_t g, int i0, Group& G) __attribute__((always_inline)) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const bool live = g + i0 + q < n;
+                G.b[q] = live ? rl64(bt.rb, i0 + q) : 0;
+                G.e[q] = live ? rl64(bt.re, i0 + q) : 0;
+                // unconditional loads (masked-off entries read the chain's dummy floats), so the
+                // compiler can count them instead of draining vmcnt around branches
+                const int64_t ka = G.b[q] + lane, kc = G.b[q] + 64 + lane;
+                const bool ia = ka < G.e[q], ic = kc < G.e[q];
+                const int32_t va = *(ia ? &COL[ka] : (gptr<int32_t>)dummy_i);
+                const S sa = *(ia ? &X[ka] : (gptr<S>)dummy_s);
+                const int32_t vc = *(ic ? &COL[kc] : (gptr<int32_t>)dummy_i);
+                const S sc = *(ic ? &X[kc] : (gptr<S>)dummy_s);
+                G.ca[q] = ia ? va : 0;
+                G.xa[q] = ia ? float(sa) : 0.0f;
+                G.cb[q] = ic ? vc : 0;
+                G.xb[q] = ic ? float(sc) : 0.0f;
+            }
+        };
+        // Stage rows g + i0 .. + 7 (those < n) from G, in phases so that the LDS round trips of
+        // the eight rows overlap (one wave's LDS operations execute in program order, so a later
+        // row's tag read still sees an earlier row's tag write without waiting for it):
+        //   D: clear the tags rows u - SR + 1 still own (their slots are reused by rows u + 1);
+        //   A: each row's tag lookups and tag writes;
+        //   B: wait until the chain is done with the slots being reused;
+        //   C: write the rows' slots (entries, correction entries, label, step), publish.
+        auto stage_group = [&](const Batch& bt, int64_t g, int i0, const Group& G) __attribute__((always_inline)) -> bool {
+            const int64_t u0 = g + i0;
+            int nq = (int)(n - u0 < 8 ? n - u0 : 8);
+            // D
+            {
+                int32_t oa[8], ob[8], on[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int64_t o = u0 + q - SR + 1;
+                    const bool live = q < nq && o >= 0;
+                    const SpecSlot& so = slots[(o + SR) % SR];
+                    on[q] = live ? so.nnz : 0;
+                    oa[q] = so.col[lane];
+                    ob[q] = so.col[lane + 64];
+                }
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int64_t o = u0 + q - SR + 1;
+                    const unsigned otag = (unsigned)(o & 255) << 8;
+                    if (lane < on[q] && tagpos[oa[q]] == (otag | (unsigned)lane)) tagpos[oa[q]] = 0xFFFF;
+                    if (lane + 64 < on[q] && tagpos[ob[q]] == (otag | (unsigned)(lane + 64))) tagpos[ob[q]] = 0xFFFF;
+                }
+            }
+            // A
+            unsigned ta[8], tc[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int64_t u = u0 + q;
+                const int nnz = q < nq ? (int)(G.e[q] - G.b[q]) : 0;
+                const unsigned tag = (unsigned)(u & 255) << 8;
+                ta[q] = 0xFFFF;
+                tc[q] = 0xFFFF;
+                if (lane < nnz) {
+                    ta[q] = tagpos[G.ca[q]];
+                    tagpos[G.ca[q]] = (uint16_t)(tag | (unsigned)lane);
+                }
+                if (lane + 64 < nnz) {
+                    tc[q] = tagpos[G.cb[q]];
+                    tagpos[G.cb[q]] = (uint16_t)(tag | (unsigned)(lane + 64));
+                }
+            }
+            // B: slot u % SR last held row u - SR, read by the chain up to row u - SR + SK
+            const int64_t need = u0 + nq - 1 - SR + SK + 1;
+            if ((int64_t)done < need) {
+                if (!spin(&hdr->done, need, 16)) return false;
+                done = __hip_atomic_load(&hdr->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            // C
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                if (q < nq) {
+                    const int64_t u = u0 + q;
+                    SpecSlot& sl = slots[u % SR];
+                    const unsigned dla = ((unsigned)u - (ta[q] >> 8)) & 255;
+                    const unsigned dlc = ((unsigned)u - (tc[q] >> 8)) & 255;
+                    const int32_t pa = (ta[q] != 0xFFFF && dla >= 1 && dla <= SK) ? (int32_t)(dla << 8 | (ta[q] & 255)) : -1;
+                    const int32_t pb = (tc[q] != 0xFFFF && dlc >= 1 && dlc <= SK) ? (int32_t)(dlc << 8 | (tc[q] & 255)) : -1;
+                    sl.col[lane] = G.ca[q];
+                    sl.col[lane + 64] = G.cb[q];
+                    sl.val[lane] = G.xa[q];
+                    sl.val[lane + 64] = G.xb[q];
+                    sl.prev[lane] = (int16_t)pa;
+                    sl.prev[lane + 64] = (int16_t)pb;
+                    if (lane == 0) {
+                        sl.nnz = (int)(G.e[q] - G.b[q]);
+                        sl.y = readlane_d(bt.y, i0 + q);
+                        sl.s = readlane_d(bt.s, i0 + q);
+                    }
+                }
+            }
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            if (nq > 0)
+                __hip_atomic_store(&hdr->ready, (unsigned)(u0 + nq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return true;
+        };
+        Batch cur = load_batch(0), nxt = load_batch(64);
+        Group GA, GB;
+        load_group(cur, 0, 0, GA);
+        for (int64_t g = 0; g < n; g += 64) {
+            bool ok = true;
+            static_for<4>([&](auto kc) {
+                // group i0 is in GA; fetch group i0 + 8 into GB, stage GA; then the same the other way
+                constexpr int i0 = 16 * decltype(kc)::value;
+                if (!ok) return;
+                load_group(cur, g, i0 + 8, GB);
+                ok = stage_group(cur, g, i0, GA);
+                if constexpr (i0 + 16 < 64) load_group(cur, g, i0 + 16, GA);
+                else load_group(nxt, g + 64, 0, GA);
+                if (ok) ok = stage_group(cur, g, i0 + 8, GB);
+            });
+            if (!ok) break;
+            cur = nxt;
+            nxt = load_batch(g + 128);
+        }
+        if (L.stamps && lane == 0) {
+            L.stamps[(size_t)chain * 4 + 2] = __builtin_amdgcn_s_memtime() - st_begin;
+            L.stamps[(size_t)chain * 4 + 3] = st_wait;
+        }
+        return;
+    }
+
+    // ---------------- chain ----------------
+    double alpha = 1.0;
+    double loss_sum = 0.0;
+    float loss_blk = 0.0f;
+    int64_t count = 0;
+    unsigned ready = 0;
+    float* dummy = V + d + lane;              // target of masked-off gathers / stores
+    float gr[SK][2];                          // gathered weights of rows t .. t + SK - 1
+    // prologue: gathers of rows 0 .. SK-1, each followed by two (dummy) stores, the same
+    // VMEM pattern as a sample of the loop
+    auto issue_gather = [&](int64_t u, float (&g)[2]) __attribute__((always_inline)) -> bool {
+        const float* pa = dummy;
+        const float* pb = dummy;
+        if (u < n) {
+            if ((int64_t)ready < u + 1) {
+                if (!spin(&hdr->ready, u + 1, 2)) return false;
+                ready = __hip_atomic_load(&hdr->ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            const SpecSlot& sl = slots[u % SR];
+            const int nnz = sl.nnz;
+            if (lane < nnz) pa = V + sl.col[lane];
+            if (lane + 64 < nnz) pb = V + sl.col[lane + 64];
+        }
+        g[0] = gather_sc1(pa);
+        g[1] = gather_sc1(pb);
+        return true;
+    };
+    bool ok = true;
+    static_for<SK>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        if (ok) ok = issue_gather(q, gr[q]);
+        store_f32(dummy, 0.0f);
+        store_f32(dummy, 0.0f);
+    });
+    // one sample; Q = t % SK (compile-time in the unrolled loop)
+    auto sample = [&](auto qc, int64_t t) __attribute__((always_inline)) -> bool {
+        constexpr int Q = decltype(qc)::value;
+        // row t's gather: issued SK samples ago, followed by 4 SK - 2 VMEM instructions
+        asm volatile("s_waitcnt vmcnt(%2)" : "+v"(gr[Q][0]), "+v"(gr[Q][1]) : "i"(4 * SK - 2) : "memory");
+        const SpecSlot& sl = slots[t % SR];
+        const int nnz = sl.nnz;
+        float w0 = gr[Q][0], w1 = gr[Q][1];
+        const float x0 = sl.val[lane], x1 = sl.val[lane + 64];
+        const int32_t p0 = sl.prev[lane], p1 = sl.prev[lane + 64];   // sign-extended
+        // features also in rows t-SK .. t-1: their stores came after this gather
+        if (p0 >= 0) w0 = slots[(t - (p0 >> 8)) % SR].nv[p0 & 255];
+        if (p1 >= 0) w1 = slots[(t - (p1 >> 8)) % SR].nv[p1 & 255];
+        if (lane >= nnz) { w0 = 0.0f; }
+        if (lane + 64 >= nnz) { w1 = 0.0f; }
+        float acc = x0 * w0;
+        acc = __builtin_fmaf(x1, w1, acc);
+        float z = wave_sum_uniform(acc);
+        const double s = sl.s;
+        if constexpr (L2) {
+            z = float(alpha * double(z));
+            alpha *= 1.0 - s * kp.reg;
+        }
+        float loss;
+        const float c = sparse_coef<GRAD>(z, float(sl.y), float(s), loss);
+        loss_blk += loss;
+        if ((t & 31) == 31) { loss_sum += double(loss_blk); loss_blk = 0.0f; }
+        count += 1;
+        const float cv = L2 ? float(double(c) / alpha) : c;
+        const float nv0 = __builtin_fmaf(cv, x0, w0);
+        const float nv1 = __builtin_fmaf(cv, x1, w1);
+        SpecSlot& slw = slots[t % SR];
+        slw.nv[lane] = nv0;
+        slw.nv[lane + 64] = nv1;
+        const int32_t c0 = sl.col[lane], c1 = sl.col[lane + 64];
+        // the gather of row t + SK, then this row's stores (2 + 2 VMEM instructions)
+        if (!issue_gather(t + SK, gr[Q])) return false;
+        store_f32(lane < nnz ? V + c0 : dummy, nv0);
+        store_f32(lane + 64 < nnz ? V + c1 : dummy, nv1);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __hip_atomic_store(&hdr->done, (unsigned)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return true;
+    };
+    for (int64_t t = 0; ok && t < n; t += SK) {
+        static_for<SK>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            if (ok && t + q < n) ok = sample(qc, t + q);
+        });
+    }
+    __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (L.stamps && lane == 0) {
+        L.stamps[(size_t)chain * 4 + 0] = __builtin_amdgcn_s_memtime() - st_begin;
+        L.stamps[(size_t)chain * 4 + 1] = st_wait;
+    }
+    loss_sum += double(loss_blk);
+    if constexpr (GRAD == G_LEAST_SQUARES) loss_sum = loss_sum / 2.0;
+    double nsq = 0.0;
+    double* wo = L.w_out + (int64_t)chain * d;
+    for (int i = lane; i < d; i += 64) {
+        const double wv = alpha * double(__hip_atomic_load(&V[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        wo[i] = wv;
+        if constexpr (L2) nsq += wv * wv;
+    }
+    double rv = 0.0;
+    if constexpr (L2) {
+        nsq = wave_sum(nsq);
+        if (count > 0) {
+            const double nrm = sqrt(nsq);
+            rv = 0.5 * kp.reg * nrm * nrm;
+        }
+    }
+    if (lane == 0) {
+        L.rv[chain] = rv;
+        L.loss[chain] = loss_sum;
+        L.cnt[chain] = count;
+        L.cnt_d[chain] = double(count);
+    }
+}
+
+size_t sparse_spec_lds_bytes(int d) {
+    return sizeof(SpecHeader) + SR * sizeof(SpecSlot) + (((size_t)d * 2 + 15) / 16) * 16;
+}
+
+bool sparse_path_applies(int layout, int compute, int updater, bool check_conv) {
+    return layout == kCsr && compute == 1 && !check_conv &&
+           (updater == U_SIMPLE || updater == U_SQUARED_L2);
+}
+
+template <typename S, int GRAD>
+static int sparse_upd(const ChainLaunch& L, const KParams& kp, int upd, hipStream_t st) {
+    if (upd == U_SIMPLE)
+        hipLaunchKernelGGL((chain_sparse<S, GRAD, U_SIMPLE>), dim3(kp.n_chains), dim3(64), 0, st, L, kp);
+    else
+        hipLaunchKernelGGL((chain_sparse<S, GRAD, U_SQUARED_L2>), dim3(kp.n_chains), dim3(64), 0, st, L, kp);
+    return (int)hipGetLastError();
+}
+
+template <typename S>
+static int sparse_grad(const ChainLaunch& L, const KParams& kp, int grad, int upd, hipStream_t st) {
+    switch (grad) {
+    case G_LOGISTIC: return sparse_upd<S, G_LOGISTIC>(L, kp, upd, st);
+    case G_LEAST_SQUARES: return sparse_upd<S, G_LEAST_SQUARES>(L, kp, upd, st);
+    case G_HINGE: return sparse_upd<S, G_HINGE>(L, kp, upd, st);
+    default: return -3;
+    }
+}
+
+template <typename S, int GRAD>
+static int spec_upd(const ChainLaunch& L, const KParams& kp, int upd, size_t lds, hipStream_t st) {
+    auto k = upd == U_SIMPLE ? chain_sparse_spec<S, GRAD, U_SIMPLE> : chain_sparse_spec<S, GRAD, U_SQUARED_L2>;
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(128), lds, st, L, kp);
+    return (int)hipGetLastError();
+}
+
+template <typename S>
+static int spec_grad(const ChainLaunch& L, const KParams& kp, int grad, int upd, size_t lds, hipStream_t st) {
+    switch (grad) {
+    case G_LOGISTIC: return spec_upd<S, G_LOGISTIC>(L, kp, upd, lds, st);
+    case G_LEAST_SQUARES: return spec_upd<S, G_LEAST_SQUARES>(L, kp, upd, lds, st);
+    case G_HINGE: return spec_upd<S, G_HINGE>(L, kp, upd, lds, st);
+    default: return -3;
+    }
+}
+
+int launch_sparse_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
+                         int updater, int64_t max_nnz, hipStream_t stream, int* kernel_variant) {
+    if (kp.n_chains <= 0) return 0;
+    if (!L.wf32 || L.wstride < (int64_t)kp.d + 128) return (int)hipErrorInvalidValue;
+    static const bool no_spec = [] {
+        const char* e = getenv("PSGD_SPARSE_NOSPEC");   // A/B measurements
+        return e && *e && *e != '0';
+    }();
+    const size_t lds = sparse_spec_lds_bytes(kp.d);
+    if (!no_spec && max_nnz <= SCAP && lds <= 160 * 1024) {
+        if (kernel_variant) *kernel_variant = 410 + storage;
+        if (storage == 1) return spec_grad<float>(L, kp, gradient, updater, lds, stream);
+        return spec_grad<double>(L, kp, gradient, updater, lds, stream);
+    }
+    if (kernel_variant) *kernel_variant = 400 + storage;
+    if (storage == 1) return sparse_grad<float>(L, kp, gradient, updater, stream);
+    return sparse_grad<double>(L, kp, gradient, updater, stream);
+}
+
+// Longest row of a CSR partition (registration of device-resident rows).
+__global__ void max_nnz_kernel(const int64_t* __restrict__ rp, int64_t n, unsigned long long* out) {
+    unsigned long long m = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const unsigned long long z = (unsigned long long)(rp[i + 1] - rp[i]);
+        m = z > m ? z : m;
+    }
+    if (m) atomicMax(out, m);
+}
+
+int csr_max_nnz(const int64_t* d_row_ptr, int64_t n, int64_t* out, hipStream_t st) {
+    *out = 0;
+    if (n <= 0) return 0;
+    unsigned long long* d = nullptr;
+    hipError_t e = hipMallocAsync((void**)&d, sizeof(unsigned long long), st);
+    if (e) return (int)e;
+    (void)hipMemsetAsync(d, 0, sizeof(unsigned long long), st);
+    hipLaunchKernelGGL(max_nnz_kernel, dim3(256), dim3(256), 0, st, d_row_ptr, n, d);
+    unsigned long long h = 0;
+    (void)hipMemcpyAsync(&h, d, sizeof h, hipMemcpyDeviceToHost, st);
+    e = hipStreamSynchronize(st);
+    (void)hipFreeAsync(d, st);
+    *out = (int64_t)h;
+    return (int)e;
+}
+
+}  // namespace psgd

@@ -63,6 +63,27 @@ class DevicePartition:
         return int(self.d)
 
 
+@dataclass
+class DeviceCsrPartition:
+    """A CSR partition already resident in HBM (torch tensors on the context's device),
+    registered zero-copy (psgd_register_csr_device): row_ptr int64 [n+1] absolute offsets into
+    col (int32, strictly increasing per row) and val (float32/float64)."""
+
+    labels: object
+    row_ptr: object
+    col: object
+    val: object
+    d: int
+
+    @property
+    def n_rows(self) -> int:
+        return int(self.labels.shape[0])
+
+    @property
+    def num_features(self) -> int:
+        return int(self.d)
+
+
 def slice_positions(n: int, num_slices: int):
     """[ext] Spark ParallelCollectionRDD.slice.positions."""
     if num_slices < 1:

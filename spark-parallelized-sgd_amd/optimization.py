@@ -24,7 +24,8 @@ from typing import List, Optional, Tuple
 import numpy as np
 
 from . import _native as N
-from .data import CsrPartition, DensePartition, DevicePartition, PartitionedData, shard_range
+from .data import (CsrPartition, DensePartition, DeviceCsrPartition, DevicePartition, PartitionedData,
+                   shard_range)
 from .gradient import Gradient, gradient_kind
 from .updater import AdamSGDUpdater, SGDUpdater, updater_kind
 
@@ -173,6 +174,11 @@ class HipEngine(ShardedEngine):
                 dt = N.F32 if part.x.dtype == self.torch.float32 else N.F64
                 self.ctx.register_dense_device(p, part.n_rows, part.d, int(part.x.stride(0)),
                                                part.labels.data_ptr(), part.x.data_ptr(), dt)
+            elif isinstance(part, DeviceCsrPartition):
+                dt = N.F32 if part.val.dtype == self.torch.float32 else N.F64
+                self.ctx.register_csr_device(p, part.n_rows, part.d, part.labels.data_ptr(),
+                                             part.row_ptr.data_ptr(), part.col.data_ptr(),
+                                             part.val.data_ptr(), dt)
             else:
                 raise IllegalArgumentException(f"unsupported partition type {type(part).__name__}")
         self.ctx.registered_token = key

@@ -1,0 +1,138 @@
+"""The fp32 CSR chain kernel (psgd_sparse.hip) against the fp64 CPU oracle.
+
+fp32 compute is the throughput mode; its stated tolerance is weights within
+FP32_REL * max|w| and the loss history within FP32_LOSS_REL relative of the fp64 oracle on the
+same inputs. Chain counts are exact.
+
+Cases: every gradient x {Simple, SquaredL2 (alpha-scaled lazy form)}; a narrow d where
+consecutive rows share features all the time (the kernel's gather after its own scatter);
+rows wider than 128 non-zeros (the per-lane loop past two entries); empty rows, empty and
+one-row partitions; sampled batches (miniBatchFraction < 1); device-resident CSR registration.
+"""
+import numpy as np
+import pytest
+
+from conftest import has_gpu
+
+pytestmark = pytest.mark.gpu
+
+FP32_REL = 2e-4
+FP32_LOSS_REL = 1e-4
+
+G = {"logistic": "LogisticGradient", "least_squares": "LeastSquaresGradient", "hinge": "HingeGradient"}
+U = {"simple": "SimpleSGDUpdater", "squared_l2": "SquaredL2SGDUpdater"}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not has_gpu():
+        pytest.skip("no GPU")
+
+
+def synth_csr(rng, n, d, kmin, kmax, grad):
+    rp, col, val = [0], [], []
+    for _ in range(n):
+        k = int(rng.integers(kmin, kmax + 1))
+        idx = np.sort(rng.choice(d, size=min(k, d), replace=False))
+        col += idx.tolist()
+        v = rng.uniform(0.1, 1.0, size=len(idx))
+        v /= max(np.linalg.norm(v), 1e-12)
+        val += v.astype(np.float32).tolist()
+        rp.append(len(col))
+    rp, col, val = np.array(rp, np.int64), np.array(col, np.int32), np.array(val, np.float64)
+    wt = rng.standard_normal(d)
+    z = np.array([val[rp[i]:rp[i + 1]] @ wt[col[rp[i]:rp[i + 1]]] for i in range(n)])
+    if grad == "least_squares":
+        y = z + 0.1 * rng.standard_normal(n)
+    else:
+        y = ((z + rng.logistic(size=n)) > 0).astype(np.float64)
+    return rp, col, val, y
+
+
+def check(pkg, oracle, rp, col, val, y, d, offs, grad, upd, step, reg, iters, frac=1.0, dtype=np.float32):
+    vstore = val.astype(dtype)
+    parts = [pkg.CsrPartition(y[a:b], rp[a:b + 1] - rp[a], col[rp[a]:rp[b]], vstore[rp[a]:rp[b]], d)
+             for a, b in zip(offs[:-1], offs[1:])]
+    data = pkg.PartitionedData(parts)
+    w, h, counts = pkg.runParallelizedSGD(data, getattr(pkg, G[grad])(), getattr(pkg, U[upd])(), step,
+                                          iters, reg, frac, np.zeros(d), 0.0, compute_dtype="f32",
+                                          return_chain_counts=True)
+    # 41x: gathers SK samples ahead (rows <= 128 non-zeros, tag table in LDS); 40x: one per sample
+    spec = int(np.max(np.diff(rp))) <= 128
+    want = (410 if spec else 400) + (1 if dtype == np.float32 else 0)
+    assert pkg.optimization.get_context(0).last_kernel() == want
+    mat = oracle.Matrix(y, row_ptr=rp, col=col, val=vstore.astype(np.float64), d=d)
+    wr, hr, cr = oracle.run(mat, offs, grad, upd, step, iters, reg, np.zeros(d), tol=0.0, fraction=frac,
+                            n_threads=8)
+    tag = f"d={d} {grad} {upd} f={frac}"
+    assert [list(c) for c in counts] == [list(c) for c in cr[: len(counts)]], tag
+    scale = max(np.max(np.abs(wr)), 1e-30)
+    err = np.max(np.abs(w - wr)) / scale
+    assert err <= FP32_REL, f"{tag}: weights max err {err:.3g} x max|w|"
+    herr = np.max(np.abs(h - hr) / np.maximum(np.abs(hr), 1e-30))
+    assert herr <= FP32_LOSS_REL, f"{tag}: loss rel err {herr:.3g}"
+
+
+@pytest.mark.parametrize("grad", ["least_squares", "logistic", "hinge"])
+@pytest.mark.parametrize("upd", ["simple", "squared_l2"])
+def test_sparse_wide(pkg, oracle, grad, upd):
+    rng = np.random.default_rng(len(grad) * 7 + len(upd))
+    n, d = 1500, 3000
+    rp, col, val, y = synth_csr(rng, n, d, 0, 40, grad)
+    offs = [0, 500, 500, 501, 1500]
+    check(pkg, oracle, rp, col, val, y, d, offs, grad, upd, 0.3, 0.05, 3)
+
+
+@pytest.mark.parametrize("grad", ["least_squares", "logistic", "hinge"])
+def test_sparse_narrow_overlapping_rows(pkg, oracle, grad):
+    # d = 12 with up to 9 non-zeros per row: nearly every feature is shared by consecutive rows
+    rng = np.random.default_rng(3 + len(grad))
+    n, d = 900, 12
+    rp, col, val, y = synth_csr(rng, n, d, 1, 9, grad)
+    offs = [0, 300, 600, 900]
+    check(pkg, oracle, rp, col, val, y, d, offs, grad, "simple", 0.2, 0.0, 3)
+    check(pkg, oracle, rp, col, val, y, d, offs, grad, "squared_l2", 0.2, 0.1, 2)
+
+
+def test_sparse_rows_wider_than_128(pkg, oracle):
+    rng = np.random.default_rng(9)
+    n, d = 400, 1000
+    rp, col, val, y = synth_csr(rng, n, d, 100, 300, "logistic")
+    check(pkg, oracle, rp, col, val, y, d, [0, 200, 400], "logistic", "simple", 0.5, 0.0, 2)
+    check(pkg, oracle, rp, col, val, y, d, [0, 200, 400], "hinge", "squared_l2", 0.5, 0.02, 2)
+
+
+def test_sparse_sampled_batches(pkg, oracle):
+    rng = np.random.default_rng(12)
+    n, d = 2000, 500
+    rp, col, val, y = synth_csr(rng, n, d, 0, 30, "hinge")
+    for frac in (0.15, 0.6):
+        check(pkg, oracle, rp, col, val, y, d, [0, 1000, 2000], "hinge", "simple", 0.5, 0.0, 3, frac=frac)
+
+
+def test_sparse_f64_storage(pkg, oracle):
+    rng = np.random.default_rng(13)
+    n, d = 800, 200
+    rp, col, val, y = synth_csr(rng, n, d, 0, 20, "logistic")
+    check(pkg, oracle, rp, col, val, y, d, [0, 400, 800], "logistic", "simple", 0.5, 0.0, 2,
+          dtype=np.float64)
+
+
+def test_sparse_device_registration(pkg, oracle):
+    import torch
+    rng = np.random.default_rng(14)
+    n, d = 1000, 700
+    rp, col, val, y = synth_csr(rng, n, d, 1, 50, "least_squares")
+    dev = torch.device("cuda", 0)
+    t_rp = torch.from_numpy(rp).to(dev)
+    t_col = torch.from_numpy(col).to(dev)
+    t_val = torch.from_numpy(val.astype(np.float32)).to(dev)
+    t_y = torch.from_numpy(y).to(dev)
+    offs = [0, 250, 1000]
+    parts = [pkg.DeviceCsrPartition(t_y[a:b], t_rp[a:b + 1], t_col, t_val, d) for a, b in zip(offs[:-1], offs[1:])]
+    w, h = pkg.runParallelizedSGD(pkg.PartitionedData(parts), pkg.LeastSquaresGradient(), pkg.SimpleSGDUpdater(),
+                                  0.3, 3, 0.0, 1.0, np.zeros(d), 0.0, compute_dtype="f32")
+    mat = oracle.Matrix(y, row_ptr=rp, col=col, val=val.astype(np.float32).astype(np.float64), d=d)
+    wr, hr, _ = oracle.run(mat, offs, "least_squares", "simple", 0.3, 3, 0.0, np.zeros(d), tol=0.0)
+    assert np.max(np.abs(w - wr)) <= FP32_REL * np.max(np.abs(wr))
+    assert np.max(np.abs(h - hr) / np.abs(hr)) <= FP32_LOSS_REL
