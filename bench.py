@@ -34,21 +34,29 @@ CSR_NNZ = 94  # c4: nonzeros per row (rcv1's mean)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def pmc_traffic(workload, grad, variant, storage):
+def pmc_traffic(workload, grad, variant, storage, rows):
     """HBM bytes per chain-kernel launch from the newest committed rocprofv3 PMC summary of the
     same workload and kernel instance (profiles/r*_<workload>_pmc.json, tools/profile_round.sh +
     tools/pmc_summary.py; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM), or None."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_pmc.json")))
-    if not files or not (300 <= variant < 400):
+    if not files or not (300 <= variant < 500):
         return None, None
     g = {"logistic": 0, "least_squares": 1, "hinge": 2}[grad]
-    prefix = f"psgd::chain_block<{'float' if storage == 'f32' else 'double'}, {g}, 0, {variant - 300},"
+    sname = "float" if storage == "f32" else "double"
+    if variant >= 410:
+        prefix = f"psgd::chain_sparse_spec<{sname}, {g}, 0>"
+    elif variant >= 400:
+        prefix = f"psgd::chain_sparse<{sname}, {g}, 0>"
+    else:
+        prefix = f"psgd::chain_block<{sname}, {g}, 0, {variant - 300},"
     with open(files[-1]) as f:
         summ = json.load(f)
     for name, e in summ.get("kernels", {}).items():
         if name.startswith(prefix) and "hbm_bytes" in e:
-            return e["hbm_bytes"], os.path.relpath(files[-1], ROOT)
+            # the summary's launch may have processed a different row count (--rows): per row
+            per_row = e["hbm_bytes"] / max(summ.get("rows_per_launch") or rows, 1)
+            return per_row * rows, os.path.relpath(files[-1], ROOT)
     return None, None
 
 
@@ -275,7 +283,7 @@ def main():
     local_samples = n
     # one chain-kernel launch processes every row of this GPU's partitions
     achieved = local_samples * bytes_per_sample / avg_kernel_s / 1e9
-    traffic, traffic_src = pmc_traffic(args.workload, grad, engine.ctx.last_kernel(), sdt)
+    traffic, traffic_src = pmc_traffic(args.workload, grad, engine.ctx.last_kernel(), sdt, n)
     out = {
         "metric": "training samples/sec (whole node) + achieved HBM GB/s, logistic SGD 1/2/4/8 GPUs",
         "value": value, "unit": "samples/s", "n_gpus": world, "steps": args.steps,

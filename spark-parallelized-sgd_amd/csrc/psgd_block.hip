@@ -534,8 +534,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
 // The Logistic loss of the chain's rows from their margins (PSGD.scala:254's lossSum; [ext] MLlib
 // 1.6.1 LogisticGradient: margin = -z, loss = y > 0 ? log1pExp(margin) : log1pExp(margin) - margin),
-// in f64, one workgroup per chain. z_t is the fp32 chain's dot for row t before its update.
-__global__ __launch_bounds__(256) void margin_loss_kernel(ChainLaunch L) {
+// in f64, one 1024-thread workgroup per chain (16 waves per CU: the f64 log1p/exp chains are
+// latency-bound per thread). z_t is the fp32 chain's dot for row t before its update.
+__global__ __launch_bounds__(1024) void margin_loss_kernel(ChainLaunch L) {
     const int chain = blockIdx.x;
     const int64_t n = L.cnt[chain];
     const double* y = L.descs[chain].y;
@@ -547,10 +548,14 @@ __global__ __launch_bounds__(256) void margin_loss_kernel(ChainLaunch L) {
         acc += as_global(y)[t] > 0.0 ? l : l - margin;
     }
     acc = wave_sum(acc);
-    __shared__ double part[4];
+    __shared__ double part[16];
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
     __syncthreads();
-    if (threadIdx.x == 0) L.loss[chain] = (part[0] + part[1]) + (part[2] + part[3]);
+    if (threadIdx.x == 0) {
+        double s = 0.0;
+        for (int k = 0; k < 16; ++k) s += part[k];
+        L.loss[chain] = s;
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -588,7 +593,7 @@ static int launch_block(const ChainLaunch& L, const KParams& kp, bool full, size
     }
     if constexpr (GRAD == G_LOGISTIC) {
         if (!L.zbuf) return (int)hipErrorInvalidValue;
-        hipLaunchKernelGGL(margin_loss_kernel, dim3(kp.n_chains), dim3(256), 0, st, L);
+        hipLaunchKernelGGL(margin_loss_kernel, dim3(kp.n_chains), dim3(1024), 0, st, L);
     }
     return (int)hipGetLastError();
 }
