@@ -159,6 +159,27 @@ int32_t psgd_ctx_last_kernel(psgd_ctx* ctx);
  * recorded around it on the launch stream (waits for that launch to finish). */
 int32_t psgd_ctx_last_chain_ms(psgd_ctx* ctx, double* ms_out);
 
+/* LIBSVM text ingest (the caller side of the path: MLUtils.loadLibSVMFile(sc, path,
+ * numFeatures, minPartitions) [ext Spark MLlib 1.6.1] building the RDD passed to
+ * runParallelizedSGD, PSGD.scala:188). Partitions follow sc.textFile(path, minPartitions) on a
+ * local file (Hadoop FileInputFormat splits, LineRecordReader line ownership); rows in file
+ * order; 1-based indices become 0-based and must be strictly increasing per line;
+ * num_features <= 0 infers max index + 1. Host arrays, freed by psgd_libsvm_free. */
+typedef struct {
+    int64_t n_rows;
+    int32_t d;
+    int32_t n_parts;
+    int64_t* part_offsets;  /* [n_parts + 1] row offsets of the partitions */
+    double* labels;         /* [n_rows] */
+    int64_t* row_ptr;       /* [n_rows + 1] */
+    int32_t* col;           /* [nnz] */
+    double* val;            /* [nnz] */
+} psgd_libsvm;
+
+int32_t psgd_libsvm_read(const char* path, int32_t num_features, int32_t min_partitions,
+                         psgd_libsvm** out);
+void psgd_libsvm_free(psgd_libsvm* data);
+
 #ifdef __cplusplus
 }
 #endif

@@ -17,6 +17,7 @@ from .optimization import (HipEngine, ParallelizedSGD, ShardedEngine, make_param
                            runParallelizedSGD)
 from .updater import (AdaGradSGDUpdater, AdamSGDUpdater, L1SGDUpdater, SGDUpdater,
                       SimpleSGDUpdater, SquaredL2SGDUpdater)
+from .util import loadLibSVMFile
 
 __all__ = [
     "ParallelizedSGD", "runParallelizedSGD", "HipEngine", "ShardedEngine", "make_params",
@@ -24,6 +25,6 @@ __all__ = [
     "SGDUpdater", "SimpleSGDUpdater", "SquaredL2SGDUpdater", "L1SGDUpdater",
     "AdaGradSGDUpdater", "AdamSGDUpdater",
     "PartitionedData", "DensePartition", "CsrPartition", "DevicePartition", "DeviceCsrPartition",
-    "shard_range",
+    "shard_range", "loadLibSVMFile",
     "IllegalArgumentException", "UnsupportedOperationException", "DeviceError", "build",
 ]

@@ -23,8 +23,15 @@ EXPORTED = (
     "psgd_register_dense", "psgd_register_csr", "psgd_register_dense_device", "psgd_register_csr_device",
     "psgd_clear_partitions", "psgd_num_partitions", "psgd_run_epoch", "psgd_run_epoch_device",
     "psgd_fold_partials_device", "psgd_convergence_terms_device", "psgd_initial_regval",
-    "psgd_ctx_last_kernel", "psgd_ctx_last_chain_ms",
+    "psgd_ctx_last_kernel", "psgd_ctx_last_chain_ms", "psgd_libsvm_read", "psgd_libsvm_free",
 )
+
+
+class psgd_libsvm(C.Structure):
+    _fields_ = [("n_rows", C.c_int64), ("d", C.c_int32), ("n_parts", C.c_int32),
+                ("part_offsets", C.POINTER(C.c_int64)), ("labels", C.POINTER(C.c_double)),
+                ("row_ptr", C.POINTER(C.c_int64)), ("col", C.POINTER(C.c_int32)),
+                ("val", C.POINTER(C.c_double))]
 
 
 class IllegalArgumentException(ValueError):
@@ -93,6 +100,8 @@ def lib():
             "psgd_initial_regval": ([vp, P, C.c_int32, vp, dp], C.c_int32),
             "psgd_ctx_last_kernel": ([vp], C.c_int32),
             "psgd_ctx_last_chain_ms": ([vp, dp], C.c_int32),
+            "psgd_libsvm_read": ([C.c_char_p, C.c_int32, C.c_int32, C.POINTER(C.POINTER(psgd_libsvm))], C.c_int32),
+            "psgd_libsvm_free": ([C.POINTER(psgd_libsvm)], None),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)

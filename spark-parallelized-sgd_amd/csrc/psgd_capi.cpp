@@ -32,6 +32,14 @@ int32_t fail(int32_t code, const std::string& msg) {
     g_last_error = msg;
     return code;
 }
+}  // namespace
+
+namespace psgd {
+// psgd_last_error() for the other translation units of the library (psgd_libsvm.cpp)
+int32_t set_error(int32_t code, const std::string& msg) { return fail(code, msg); }
+}  // namespace psgd
+
+namespace {
 
 #define HIP_TRY(expr)                                                                        \
     do {                                                                                     \

@@ -305,3 +305,31 @@ def test_determinism_many_chains(pkg):
     w1, h1 = pkg.runParallelizedSGD(data, *args)
     w2, h2 = pkg.runParallelizedSGD(data, *args)
     assert np.array_equal(w1, w2) and np.array_equal(h1, h2)
+
+
+def test_libsvm_file_to_chains(pkg, oracle, tmp_path):
+    """MLUtils.loadLibSVMFile -> runParallelizedSGD: the natively parsed CSR partitions through
+    the fp64 chain, against the oracle on the same rows and partition boundaries."""
+    rng = np.random.default_rng(21)
+    lines = []
+    for _ in range(600):
+        idx = np.sort(rng.choice(40, size=int(rng.integers(1, 8)), replace=False)) + 1
+        lines.append(f"{int(rng.integers(0, 2))} " + " ".join(f"{i}:{rng.uniform(0, 1):.5f}" for i in idx))
+    f = tmp_path / "train.libsvm"
+    f.write_text("\n".join(lines) + "\n")
+    data = pkg.loadLibSVMFile(str(f), -1, 3)
+    assert len(data.partitions) >= 3
+    w, h = pkg.runParallelizedSGD(data, pkg.HingeGradient(), pkg.SquaredL2SGDUpdater(), 0.5, 3, 0.01, 1.0,
+                                  np.zeros(data.partitions[0].d), 0.0)
+    y = np.concatenate([p.labels for p in data.partitions])
+    rp, col, val, offs = [0], [], [], [0]
+    for p in data.partitions:
+        col.append(p.col)
+        val.append(p.val)
+        rp += list(p.row_ptr[1:] + rp[-1])
+        offs.append(offs[-1] + p.n_rows)
+    mat = oracle.Matrix(y, row_ptr=np.array(rp), col=np.concatenate(col), val=np.concatenate(val),
+                        d=data.partitions[0].d)
+    wr, hr, _ = oracle.run(mat, offs, "hinge", "squared_l2", 0.5, 3, 0.01, np.zeros(data.partitions[0].d), tol=0.0)
+    assert_close(w, wr, what="weights")
+    assert_close(h, hr, what="loss")
