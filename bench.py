@@ -29,8 +29,12 @@ WORKLOADS = {
            "Logistic regression, dense 100M x 1024 (per-GPU shard: 12.5M rows, 256 of 2048 chains)"),
     "c4": ("hinge", 20_000_000, 47_236, 256, 1.0, "f32",
            "Hinge-loss linear SVM, sparse CSR rcv1-like (47,236 features, 94 nnz/row = 0.2%)"),
+    "c5": ("logistic", 125_000_000, 1 << 22, 1024, 0.5, "f32",
+           "L2 logistic regression, sparse 2^22 features (HBM-resident weights), 1B rows over 8 GPUs: "
+           "per-GPU shard 125M rows, 1024 of 8192 chains, lambda 1e-6"),
 }
-CSR_NNZ = 94  # c4: nonzeros per row (rcv1's mean)
+CSR_NNZ = {"c4": 94, "c5": 100}  # nonzeros per row (c4: rcv1's mean; c5: SURVEY §8d)
+REG = {"c5": 1e-6}                # SquaredL2 regParam (c5); others: Simple updater
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
@@ -106,7 +110,7 @@ def make_shard(torch, dev, n, d, P, grad, dtype, seed):
     return X, y, offs
 
 
-def make_csr_shard(torch, dev, n, d, P, grad, dtype, seed, nnz=CSR_NNZ):
+def make_csr_shard(torch, dev, n, d, P, grad, dtype, seed, nnz):
     """Synthetic rcv1-like CSR rows in HBM: nnz distinct sorted indices per
     row (one uniform draw in each of nnz equal column buckets), values U(0,1) L2-normalised per
     row, labels y = 1{w*.x + Logistic(0,1) > 0} from a planted w* ~ N(0,1)."""
@@ -205,9 +209,10 @@ def main():
     grad, n, d, P, step, sdt, cfg_name = WORKLOADS[args.workload]
     if args.rows:
         n = args.rows
-    csr = args.workload == "c4"
+    csr = args.workload in CSR_NNZ
     if csr:
-        rp, col, val, y, offs = make_csr_shard(torch, dev, n, d, P, grad, sdt, 1000 + rank)
+        rp, col, val, y, offs = make_csr_shard(torch, dev, n, d, P, grad, sdt, 1000 + rank,
+                                               CSR_NNZ[args.workload])
         torch.cuda.synchronize()
         parts = [pkg.DeviceCsrPartition(y[a:b], rp[a:b + 1], col, val, d) for a, b in zip(offs[:-1], offs[1:])]
         empty = lambda: pkg.DeviceCsrPartition(y[:0], rp[:1], col, val, d)
@@ -226,7 +231,9 @@ def main():
     engine = pkg.HipEngine(data, rank, world, device=local)
     gcls = {"least_squares": pkg.LeastSquaresGradient, "logistic": pkg.LogisticGradient,
             "hinge": pkg.HingeGradient}[grad]()
-    params = pkg.make_params(gcls, pkg.SimpleSGDUpdater(), step, 0.0, 1.0, 0.0, args.compute)
+    reg = REG.get(args.workload, 0.0)
+    ucls = pkg.SquaredL2SGDUpdater() if reg > 0 else pkg.SimpleSGDUpdater()
+    params = pkg.make_params(gcls, ucls, step, reg, 1.0, 0.0, args.compute)
     import numpy as np
     w = engine.weights(np.zeros(d))
     stream = engine.stream  # the engine's kernels and copies all run on this stream
@@ -277,7 +284,7 @@ def main():
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
     es = 4 if sdt == "f32" else 8
     if csr:  # values + int32 columns + int64 row pointer + f64 label (weights: L2/MALL-resident)
-        bytes_per_sample = CSR_NNZ * (es + 4) + 8 + 8
+        bytes_per_sample = CSR_NNZ[args.workload] * (es + 4) + 8 + 8
     else:
         bytes_per_sample = (d + 1) * es  # row + label (weights are on chip)
     local_samples = n
@@ -291,7 +298,8 @@ def main():
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": args.compute, "data": "synthetic (device-generated, resident in HBM)",
         "config": {"workload": f"{args.workload}: {cfg_name}", "rows_per_gpu": n, "d": d,
-                   "chains_per_gpu": P, "storage": sdt, "gradient": grad, "updater": "simple",
+                   "chains_per_gpu": P, "storage": sdt, "gradient": grad,
+                   "updater": "squared_l2" if reg > 0 else "simple", "reg_param": reg,
                    "step_size": step, "convergence_tol": 0.0, "mini_batch_fraction": 1.0,
                    "parallelism": f"dp{world} (chains sharded, RCCL all-gather + fold per epoch)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -305,7 +313,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(grad, d, P, step, args.cpu_seconds,
-                                           csr_nnz=CSR_NNZ if csr else 0)
+                                           csr_nnz=CSR_NNZ[args.workload] if csr else 0)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
