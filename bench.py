@@ -82,6 +82,8 @@ def parse():
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--compute", default="f32", choices=["f32", "f64"])
     ap.add_argument("--rows", type=int, default=0, help="override rows per GPU (testing)")
+    ap.add_argument("--fraction", type=float, default=1.0,
+                    help="miniBatchFraction: batch i = RDD.sample(false, f, 42 + i) per partition")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -233,7 +235,7 @@ def main():
             "hinge": pkg.HingeGradient}[grad]()
     reg = REG.get(args.workload, 0.0)
     ucls = pkg.SquaredL2SGDUpdater() if reg > 0 else pkg.SimpleSGDUpdater()
-    params = pkg.make_params(gcls, ucls, step, reg, 1.0, 0.0, args.compute)
+    params = pkg.make_params(gcls, ucls, step, reg, args.fraction, 0.0, args.compute)
     import numpy as np
     w = engine.weights(np.zeros(d))
     stream = engine.stream  # the engine's kernels and copies all run on this stream
@@ -276,8 +278,11 @@ def main():
         elapsed = float(t.item())
     # `cnt` is the whole job's sample count of the step (the fold sums counts over all ranks)
     samples_per_step = cnt
+    if args.fraction >= 1.0:
+        assert samples_per_step == n * world, (samples_per_step, n * world)
+    else:  # sampled batches differ per step: the timed steps' samples
+        samples_per_step = total / args.steps
     value = samples_per_step * args.steps / elapsed
-    assert samples_per_step == n * world, (samples_per_step, n * world)
     assert np.isfinite(loss), loss
     epoch_ms = [a.elapsed_time(b) for a, b in events]
     avg_epoch_s = sum(epoch_ms) / len(epoch_ms) / 1e3
@@ -287,8 +292,8 @@ def main():
         bytes_per_sample = CSR_NNZ[args.workload] * (es + 4) + 8 + 8
     else:
         bytes_per_sample = (d + 1) * es  # row + label (weights are on chip)
-    local_samples = n
-    # one chain-kernel launch processes every row of this GPU's partitions
+    local_samples = n if args.fraction >= 1.0 else samples_per_step / world
+    # one chain-kernel launch processes every (sampled) row of this GPU's partitions
     achieved = local_samples * bytes_per_sample / avg_kernel_s / 1e9
     traffic, traffic_src = pmc_traffic(args.workload, grad, engine.ctx.last_kernel(), sdt, n)
     out = {
@@ -300,7 +305,7 @@ def main():
         "config": {"workload": f"{args.workload}: {cfg_name}", "rows_per_gpu": n, "d": d,
                    "chains_per_gpu": P, "storage": sdt, "gradient": grad,
                    "updater": "squared_l2" if reg > 0 else "simple", "reg_param": reg,
-                   "step_size": step, "convergence_tol": 0.0, "mini_batch_fraction": 1.0,
+                   "step_size": step, "convergence_tol": 0.0, "mini_batch_fraction": args.fraction,
                    "parallelism": f"dp{world} (chains sharded, RCCL all-gather + fold per epoch)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -159,6 +159,15 @@ int32_t psgd_ctx_last_kernel(psgd_ctx* ctx);
  * recorded around it on the launch stream (waits for that launch to finish). */
 int32_t psgd_ctx_last_chain_ms(psgd_ctx* ctx, double* ms_out);
 
+/* The device sampler of one partition, alone: RDD.sample(false, fraction, .) over a partition
+ * of n rows whose PartitionwiseSampledRDD seed is `seed` (the partition's java.util.Random
+ * nextLong, before hashSeed) [ext Spark 1.6.1 BernoulliSampler] -- the batch selection
+ * psgd_run_epoch does for miniBatchFraction < 1 (PSGD.scala:242). Writes the kept row indices
+ * in iterator order to rows_out[0..*m_out) (rows_out holds n entries). Same contract as
+ * oracle/or_sample_partition. */
+int32_t psgd_sample_partition(int32_t device, int64_t seed, int64_t n, double fraction, int32_t* rows_out,
+                              int64_t* m_out);
+
 /* LIBSVM text ingest (the caller side of the path: MLUtils.loadLibSVMFile(sc, path,
  * numFeatures, minPartitions) [ext Spark MLlib 1.6.1] building the RDD passed to
  * runParallelizedSGD, PSGD.scala:188). Partitions follow sc.textFile(path, minPartitions) on a

@@ -24,6 +24,7 @@ EXPORTED = (
     "psgd_clear_partitions", "psgd_num_partitions", "psgd_run_epoch", "psgd_run_epoch_device",
     "psgd_fold_partials_device", "psgd_convergence_terms_device", "psgd_initial_regval",
     "psgd_ctx_last_kernel", "psgd_ctx_last_chain_ms", "psgd_libsvm_read", "psgd_libsvm_free",
+    "psgd_sample_partition",
 )
 
 
@@ -102,6 +103,7 @@ def lib():
             "psgd_ctx_last_chain_ms": ([vp, dp], C.c_int32),
             "psgd_libsvm_read": ([C.c_char_p, C.c_int32, C.c_int32, C.POINTER(C.POINTER(psgd_libsvm))], C.c_int32),
             "psgd_libsvm_free": ([C.POINTER(psgd_libsvm)], None),
+            "psgd_sample_partition": ([C.c_int32, C.c_int64, C.c_int64, C.c_double, vp, i64p], C.c_int32),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -120,6 +122,17 @@ def check(rc: int) -> None:
     if rc == PSGD_EUNSUPPORTED:
         raise UnsupportedOperationException(msg)
     raise DeviceError(f"libpsgd error {rc}: {msg}")
+
+
+def sample_partition(seed: int, n: int, fraction: float, device: int = 0):
+    """Row indices RDD.sample(false, fraction, .) keeps from an n-row partition whose sampler
+    seed is `seed`, selected on the device (psgd_sample_partition)."""
+    import numpy as np
+    rows = np.empty(max(int(n), 1), dtype=np.int32)
+    m = C.c_int64()
+    check(lib().psgd_sample_partition(device, int(seed), int(n), float(fraction), rows.ctypes.data,
+                                      C.byref(m)))
+    return rows[: m.value].copy()
 
 
 class Context:

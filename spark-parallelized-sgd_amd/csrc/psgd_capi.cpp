@@ -786,6 +786,43 @@ int32_t psgd_initial_regval(psgd_ctx* ctx, const psgd_params* params, int32_t d,
     return PSGD_OK;
 }
 
+int32_t psgd_sample_partition(int32_t device, int64_t seed, int64_t n, double fraction, int32_t* rows_out,
+                              int64_t* m_out) {
+    if (!m_out || (n > 0 && !rows_out)) return fail(PSGD_EINVAL, "rows_out/m_out is null");
+    if (n < 0 || n > INT32_MAX) return fail(PSGD_EINVAL, "n out of range");
+    *m_out = 0;
+    if (fraction <= 0.0 || n == 0) return PSGD_OK;
+    if (fraction >= 1.0) {
+        for (int64_t t = 0; t < n; ++t) rows_out[t] = (int32_t)t;
+        *m_out = n;
+        return PSGD_OK;
+    }
+    DeviceGuard g(device);
+    DevBuf desc, out, rows, xs;
+    struct Release {
+        DevBuf* b[4];
+        ~Release() {
+            for (DevBuf* x : b) x->release();
+        }
+    } release{{&desc, &out, &rows, &xs}};
+    HIP_TRY(desc.ensure(sizeof(psgd::ChainDesc)));
+    HIP_TRY(out.ensure(sizeof(psgd::ChainDesc)));
+    HIP_TRY(rows.ensure((size_t)n * sizeof(int32_t)));
+    HIP_TRY(xs.ensure(sizeof(uint64_t)));
+    psgd::ChainDesc c{};
+    c.n_rows = n;
+    const uint64_t s0 = (uint64_t)sampling::xorshift_hash_seed(seed);
+    HIP_TRY(hipMemcpy(desc.p, &c, sizeof c, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(xs.p, &s0, sizeof s0, hipMemcpyHostToDevice));
+    if (psgd::launch_sample(desc.as<psgd::ChainDesc>(), out.as<psgd::ChainDesc>(), xs.as<uint64_t>(), fraction,
+                            rows.as<int32_t>(), nullptr, n, 1, nullptr))
+        return fail(PSGD_EDEVICE, "sample kernel launch failed");
+    HIP_TRY(hipMemcpy(&c, out.p, sizeof c, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(rows_out, rows.p, (size_t)c.n_rows * sizeof(int32_t), hipMemcpyDeviceToHost));
+    *m_out = c.n_rows;
+    return PSGD_OK;
+}
+
 int32_t psgd_ctx_last_kernel(psgd_ctx* ctx) { return ctx ? ctx->last_variant : 0; }
 
 int32_t psgd_ctx_last_chain_ms(psgd_ctx* ctx, double* ms_out) {

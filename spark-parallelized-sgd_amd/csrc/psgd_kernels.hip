@@ -728,16 +728,70 @@ int launch_sq_terms(const double* a, const double* b, int d, double* out2, hipSt
 
 // ------------------------------------------------------------------------------------------
 // Bernoulli sampling of one epoch's batch ([ext] Spark 1.6.1 BernoulliSampler on an
-// XORShiftRandom, restated in oracle/psgd_oracle.c or_sample_partition): one lane per chain
-// walks its partition in iterator order. fraction <= 0.4: GapSamplingIterator (geometric skips,
-// u = max(nextDouble, 5e-11), k = (int)(log(u) / log1p(-f)), a skip before the first row and
-// after every returned row); else the filter nextDouble() <= fraction.
+// XORShiftRandom, restated in oracle/psgd_oracle.c or_sample_partition). fraction <= 0.4:
+// GapSamplingIterator (geometric skips, u = max(nextDouble, 5e-11), k = (int)(log(u) /
+// log1p(-f)), a skip before the first row and after every returned row); else the filter
+// nextDouble() <= fraction per row, in iterator order.
+//
+// The reference walks one XORShift sequence per partition; a lane doing the same is bound by
+// one dependent label load per row (~20 ms for 40k-row partitions). Both samplers consume
+// exactly two XORShift steps per draw (one nextDouble), and XORShift is linear over GF(2), so
+// draw j's state is D^j s0 with D the 64x64 bit matrix of two steps. One workgroup per
+// partition: thread i owns draws [r + 64 i, r + 64 i + 64) of round r (16384 draws a round),
+// reaching its first state through the jump matrices D^(64 * 2^k) (built at compile time),
+// and an exclusive scan over threads places its output: the filter's kept-row counts, or
+// the gap sampler's positions (pos_j = sum_{i<=j} k_i + j, strictly increasing, so the
+// emitted rows are exactly the draws with pos_j < n_rows and row j lands at index j).
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ int32_t xs_next(uint64_t& st, int bits) {
-    uint64_t x = st;
+namespace {
+struct Gf2Mat {
+    uint64_t c[64];   // column b = D * e_b
+};
+constexpr uint64_t xs_step(uint64_t x) {
     x ^= x << 21;
     x ^= x >> 35;
     x ^= x << 4;
+    return x;
+}
+constexpr uint64_t gf2_apply_c(const Gf2Mat& m, uint64_t s) {
+    uint64_t r = 0;
+    for (int b = 0; b < 64; ++b)
+        if ((s >> b) & 1) r ^= m.c[b];
+    return r;
+}
+constexpr Gf2Mat gf2_square(const Gf2Mat& m) {
+    Gf2Mat r{};
+    for (int b = 0; b < 64; ++b) r.c[b] = gf2_apply_c(m, m.c[b]);
+    return r;
+}
+constexpr int kSampThreads = 256;
+constexpr int kSampDraws = 64;   // draws per thread per round (a power of two: D^64 by squaring)
+struct SampleJumps {
+    Gf2Mat j[9];   // j[k] = D^(64 * 2^k): k < 8 place thread i, j[8] advances a round
+};
+constexpr SampleJumps make_sample_jumps() {
+    Gf2Mat d{};
+    for (int b = 0; b < 64; ++b) d.c[b] = xs_step(xs_step(1ull << b));
+    for (int i = 0; i < 6; ++i) d = gf2_square(d);
+    SampleJumps s{};
+    s.j[0] = d;
+    for (int k = 1; k < 9; ++k) s.j[k] = gf2_square(s.j[k - 1]);
+    return s;
+}
+static_assert(kSampThreads == 256 && kSampDraws == 64, "jump table is built for 256 x 64 draws");
+}  // namespace
+
+__constant__ SampleJumps kSampleJumps = make_sample_jumps();
+
+__device__ __forceinline__ uint64_t gf2_apply(const Gf2Mat& m, uint64_t s) {
+    uint64_t r = 0;
+#pragma unroll 16
+    for (int b = 0; b < 64; ++b) r ^= m.c[b] & (0ull - ((s >> b) & 1));
+    return r;
+}
+
+__device__ __forceinline__ int32_t xs_next(uint64_t& st, int bits) {
+    const uint64_t x = xs_step(st);
     st = x;
     return (int32_t)(x & ((1ull << bits) - 1));
 }
@@ -746,55 +800,117 @@ __device__ __forceinline__ double xs_next_double(uint64_t& st) {
     const int64_t b = xs_next(st, 27);
     return (double)((a << 27) + b) * 0x1.0p-53;
 }
+// GapSamplingIterator's skip for one draw
+__device__ __forceinline__ int64_t gap_skip(uint64_t& st, double lnq) {
+    double u = xs_next_double(st);
+    if (u < 5e-11) u = 5e-11;
+    const double q = log(u) / lnq;
+    return q >= 2147483647.0 ? 2147483647 : (int64_t)q;
+}
 
-__global__ __launch_bounds__(64) void sample_kernel(const ChainDesc* __restrict__ base,
-                                                    ChainDesc* __restrict__ out,
-                                                    const uint64_t* __restrict__ xs_state,
-                                                    double fraction, int32_t* __restrict__ rows,
-                                                    double* __restrict__ ys, int64_t stride, int n) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n) return;
+// Exclusive scan of v over the workgroup; *total gets the sum. sh holds kSampThreads entries.
+__device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t* sh, int64_t* total) {
+    const int tid = threadIdx.x;
+    sh[tid] = v;
+    __syncthreads();
+    for (int off = 1; off < kSampThreads; off <<= 1) {
+        const int64_t t = tid >= off ? sh[tid - off] : 0;
+        __syncthreads();
+        sh[tid] += t;
+        __syncthreads();
+    }
+    const int64_t incl = sh[tid];
+    *total = sh[kSampThreads - 1];
+    __syncthreads();
+    return incl - v;
+}
+
+__global__ __launch_bounds__(kSampThreads) void sample_kernel(const ChainDesc* __restrict__ base,
+                                                              ChainDesc* __restrict__ out,
+                                                              const uint64_t* __restrict__ xs_state,
+                                                              double fraction, int32_t* __restrict__ rows,
+                                                              double* __restrict__ ys, int64_t stride) {
+    __shared__ int64_t sh[kSampThreads];
+    __shared__ int sh_emit;
+    const int c = blockIdx.x;
+    const int tid = threadIdx.x;
     ChainDesc dsc = base[c];
-    uint64_t st = xs_state[c];
     int32_t* r = rows + (int64_t)c * stride;
-    double* yo = ys + (int64_t)c * stride;
-    const gptr<double> Y = as_global(dsc.y);
+    double* yo = ys ? ys + (int64_t)c * stride : nullptr;
+    const double* Y = dsc.y;
     const int64_t nr = dsc.n_rows;
+    uint64_t st = xs_state[c];
+#pragma unroll 1
+    for (int k = 0; k < 8; ++k)
+        if ((tid >> k) & 1) st = gf2_apply(kSampleJumps.j[k], st);
+    constexpr int64_t kRound = (int64_t)kSampThreads * kSampDraws;
     int64_t m = 0;
     if (fraction <= 0.4) {
         const double lnq = log1p(-fraction);
-        int64_t pos = 0;
-        for (;;) {
-            double u = xs_next_double(st);
-            if (u < 5e-11) u = 5e-11;
-            const double q = log(u) / lnq;
-            pos += q >= 2147483647.0 ? 2147483647 : (int64_t)q;
-            if (pos >= nr) break;
-            r[m] = (int32_t)pos;
-            yo[m] = Y[pos];
-            ++m;
-            pos += 1;
+        int64_t pos_round = 0;   // the position before the round's first draw
+        for (int64_t draw0 = 0;; draw0 += kRound) {
+            uint64_t s = st;
+            int64_t adv = 0;
+            for (int j = 0; j < kSampDraws; ++j) adv += gap_skip(s, lnq) + 1;
+            int64_t total;
+            int64_t pos = pos_round + block_excl_scan(adv, sh, &total);
+            if (tid == 0) sh_emit = 0;
+            __syncthreads();
+            s = st;
+            int emitted = 0;
+            const int64_t j0 = draw0 + (int64_t)tid * kSampDraws;
+            for (int j = 0; j < kSampDraws; ++j) {
+                pos += gap_skip(s, lnq);
+                if (pos >= nr) break;
+                r[j0 + j] = (int32_t)pos;
+                if (yo) yo[j0 + j] = Y[pos];
+                ++emitted;
+                pos += 1;
+            }
+            atomicAdd(&sh_emit, emitted);
+            __syncthreads();
+            const int64_t e = sh_emit;
+            pos_round += total;
+            if (e < kRound) {   // a draw reached n_rows: the emitted draws are a prefix
+                m = draw0 + e;
+                break;
+            }
+            st = gf2_apply(kSampleJumps.j[8], st);
+            __syncthreads();   // sh_emit is reset next round
         }
     } else {
-        for (int64_t t = 0; t < nr; ++t) {
-            if (xs_next_double(st) <= fraction) {
-                r[m] = (int32_t)t;
-                yo[m] = Y[t];
-                ++m;
+        for (int64_t draw0 = 0; draw0 < nr; draw0 += kRound) {
+            uint64_t s = st;
+            uint64_t keep = 0;
+            const int64_t t0 = draw0 + (int64_t)tid * kSampDraws;
+            for (int j = 0; j < kSampDraws; ++j)
+                if (xs_next_double(s) <= fraction && t0 + j < nr) keep |= 1ull << j;
+            int64_t total;
+            int64_t o = m + block_excl_scan(__popcll(keep), sh, &total);
+            while (keep) {
+                const int j = __ffsll((unsigned long long)keep) - 1;
+                keep &= keep - 1;
+                r[o] = (int32_t)(t0 + j);
+                if (yo) yo[o] = Y[t0 + j];
+                ++o;
             }
+            m += total;
+            st = gf2_apply(kSampleJumps.j[8], st);
         }
     }
-    dsc.rows = r;
-    dsc.y = yo;
-    dsc.n_rows = m;
-    out[c] = dsc;
+    if (tid == 0) {
+        dsc.rows = r;
+        if (yo) dsc.y = yo;
+        dsc.n_rows = m;
+        out[c] = dsc;
+    }
 }
 
 int launch_sample(const ChainDesc* base, ChainDesc* out, const uint64_t* xs_state, double fraction,
                   int32_t* rows, double* ys, int64_t stride, int n_chains, hipStream_t stream) {
     if (n_chains <= 0) return 0;
-    hipLaunchKernelGGL(sample_kernel, dim3((unsigned)((n_chains + 63) / 64)), dim3(64), 0, stream,
-                       base, out, xs_state, fraction, rows, ys, stride, n_chains);
+    hipLaunchKernelGGL(sample_kernel, dim3((unsigned)n_chains), dim3(kSampThreads), 0, stream, base, out,
+                       xs_state, fraction, rows, ys, stride);
     return (int)hipGetLastError();
 }
 

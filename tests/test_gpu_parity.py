@@ -244,6 +244,39 @@ def test_mini_batch_fraction(pkg, oracle):
         assert_close(h, hr, rel=FP32_LOSS_REL, what="fp32 loss")
 
 
+@pytest.mark.parametrize("fraction", [1e-9, 0.001, 0.1, 0.4, 0.4000001, 0.75, 0.999999])
+def test_device_sampler_matches_oracle(pkg, oracle, fraction):
+    """The device sampler (jump-ahead over the XORShift sequence, 16384 draws a round) selects
+    exactly the rows the sequential restatement of BernoulliSampler does: partitions smaller
+    than one round, exactly one round, and many rounds; both samplers (gap <= 0.4 < filter)."""
+    native = pkg._native
+    seeds = oracle.partition_seeds(42 + 3, 4)
+    for n, seed in zip((1, 16384, 16385, 1_000_003), seeds):
+        got = native.sample_partition(int(seed), n, fraction)
+        want = oracle.sample_partition(int(seed), n, fraction)
+        assert got.shape == want.shape, (n, fraction, got.shape, want.shape)
+        assert np.array_equal(got, want), (n, fraction)
+    assert native.sample_partition(7, 0, fraction).size == 0
+
+
+def test_sampled_epoch_large_partitions(pkg, oracle):
+    """Sampled epochs over partitions of several sampler rounds through the fp64 chain: chain
+    counts exact, weights at the fp64 tolerance."""
+    rng = np.random.default_rng(21)
+    X, y = synth(rng, 90_000, 8, "least_squares")
+    offs = [0, 40_000, 40_001, 90_000]
+    parts = [pkg.DensePartition(y[a:b], X[a:b]) for a, b in zip(offs[:-1], offs[1:])]
+    data = pkg.PartitionedData(parts)
+    for frac in (0.05, 0.6):
+        w, h, counts = pkg.runParallelizedSGD(data, pkg.LeastSquaresGradient(), pkg.SimpleSGDUpdater(), 0.01,
+                                              2, 0.0, frac, np.zeros(8), 0.0, return_chain_counts=True)
+        wr, hr, cr = oracle.run(oracle.Matrix(y, X), offs, "least_squares", "simple", 0.01, 2, 0.0,
+                                np.zeros(8), tol=0.0, fraction=frac)
+        assert [list(map(int, c)) for c in counts] == [list(map(int, c)) for c in cr]
+        assert_close(w, wr, what=f"f={frac} weights")
+        assert_close(h, hr, what=f"f={frac} loss")
+
+
 def test_empty_partitions_nan_poisoning(pkg, oracle):
     """Two leading empty partitions: (w*0 + w*0)/0 = NaN, as the reference's combiner gives when
     Spark merges them first (ParallelizedSGD.scala:272-274)."""
