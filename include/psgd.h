@@ -73,6 +73,10 @@ typedef struct {
                                    partition (BernoulliSampler [ext Spark 1.6.1]); 1 = every row */
     double convergence_tol;     /* [0, 1]; 0 disables the per-sample break (PSGD.scala:262) */
     double adam_beta, adam_gamma, adam_eps; /* AdamSGDUpdater(beta, gamma, eps), UPD:241-244 */
+    int32_t num_classes;        /* LogisticGradient(numClasses) [ext MLlib 1.6.1]: <= 2 binary;
+                                   K > 2 multinomial, weights of (K - 1) * d (class blocks of d),
+                                   every weight-sized buffer of the epoch calls is (K - 1) * d;
+                                   fp64 compute only */
 } psgd_params;
 
 int32_t psgd_abi_version(void);

@@ -34,7 +34,7 @@ class _Params(C.Structure):
         ("gradient", C.c_int32), ("updater", C.c_int32), ("step_size", C.c_double),
         ("reg_param", C.c_double), ("convergence_tol", C.c_double),
         ("adam_beta", C.c_double), ("adam_gamma", C.c_double), ("adam_eps", C.c_double),
-        ("mini_batch_fraction", C.c_double),
+        ("mini_batch_fraction", C.c_double), ("num_classes", C.c_int32),
     ]
 
 
@@ -107,9 +107,10 @@ class Matrix:
 
 
 def params(gradient, updater, step, reg=0.0, tol=0.001, beta=0.9, gamma=0.999, eps=1e-8,
-           fraction=1.0):
+           fraction=1.0, num_classes=2):
     p = _Params()
     p.mini_batch_fraction = fraction
+    p.num_classes = num_classes
     p.gradient = GRAD[gradient] if isinstance(gradient, str) else int(gradient)
     p.updater = UPD[updater] if isinstance(updater, str) else int(updater)
     p.step_size, p.reg_param, p.convergence_tol = step, reg, tol
@@ -117,15 +118,22 @@ def params(gradient, updater, step, reg=0.0, tol=0.001, beta=0.9, gamma=0.999, e
     return p
 
 
+def weight_dim(d, gradient, num_classes=2):
+    g = GRAD[gradient] if isinstance(gradient, str) else int(gradient)
+    return (num_classes - 1) * d if g == GRAD["logistic"] and num_classes > 2 else d
+
+
 def run(mat: Matrix, part_offsets, gradient, updater, step, iters, reg, w0, tol=0.001,
         groups=None, n_threads=1, **kw):
     """ParallelizedSGD.runParallelizedSGD restated (fraction=... sets miniBatchFraction).
-    Returns (weights, loss_history, chain_counts[iters_run, P])."""
+    Returns (weights, loss_history, chain_counts[iters_run, P]). num_classes=K > 2 selects the
+    multinomial LogisticGradient (weights of (K - 1) * d)."""
     L = lib()
     offs = np.ascontiguousarray(part_offsets, dtype=np.int64)
     P = len(offs) - 1
     w0 = np.ascontiguousarray(w0, dtype=np.float64)
-    w_out = np.zeros(mat.d, dtype=np.float64)
+    w_out = np.zeros(weight_dim(mat.d, gradient, kw.get("num_classes", 2)), dtype=np.float64)
+    assert w0.size == w_out.size, (w0.size, w_out.size)
     hist = np.zeros(max(iters, 1), dtype=np.float64)
     nh = C.c_int32(0)
     counts = np.zeros((max(iters, 1), max(P, 1)), dtype=np.int64)
@@ -151,7 +159,8 @@ def run_chains(mat: Matrix, part_offsets, gradient, updater, step, reg, w_in, to
     offs = np.ascontiguousarray(part_offsets, dtype=np.int64)
     P = len(offs) - 1
     w_in = np.ascontiguousarray(w_in, dtype=np.float64)
-    w = np.zeros((P, mat.d), dtype=np.float64)
+    w = np.zeros((P, weight_dim(mat.d, gradient, kw.get("num_classes", 2))), dtype=np.float64)
+    assert w_in.size == w.shape[1], (w_in.size, w.shape)
     rv = np.zeros(P)
     loss = np.zeros(P)
     cnt = np.zeros(P, dtype=np.int64)

@@ -96,6 +96,78 @@ typedef struct {
     const double* val;
 } row_t;
 
+int32_t or_weight_dim(int32_t d, const or_params* prm) {
+    if (prm->gradient == OR_GRAD_LOGISTIC && prm->num_classes > 2) return (prm->num_classes - 1) * d;
+    return d;
+}
+
+/* Double.toInt (Java d2i): NaN -> 0, saturating, truncation toward zero. */
+static int32_t java_d2i(double x) {
+    if (x != x) return 0;
+    if (x >= 2147483647.0) return 2147483647;
+    if (x <= -2147483648.0) return (int32_t)(-2147483647 - 1);
+    return (int32_t)x;
+}
+
+/* [ext] MLlib 1.6.1 LogisticGradient.compute(data, label, weights) for numClasses > 2: the
+ * multinomial model with class 0 as pivot; weights are numClasses - 1 blocks of dataSize.
+ * Margins over data.foreachActive skipping value == 0.0; the sum of exponentials shifted by
+ * maxMargin when it is positive (the max class contributing exp(-maxMargin) for the pivot);
+ * multiplier_i = exp(margin_i) / (sum + 1.0) - [label != 0 && label == i + 1];
+ * cumGradient(i * dataSize + index) += multiplier_i * value over the non-zero values;
+ * loss = log1p(sum) (- marginY when label > 0) (+ maxMargin when it is positive). The gradient
+ * is dense (Vectors.zeros(weights.size)). margins holds numClasses - 1 doubles of scratch. */
+static double multinomial_compute(int32_t K, const row_t* r, double label, const double* w,
+                                  grad_t* out, double* margins) {
+    const int32_t d = r->d, C1 = K - 1;
+    const int32_t ly = java_d2i(label) - 1;   /* label.toInt - 1 */
+    double marginY = 0.0, maxMargin = -INFINITY;
+    int32_t maxMarginIndex = 0;
+    for (int32_t i = 0; i < C1; ++i) {
+        const double* wi = w + (size_t)i * (size_t)d;
+        double margin = 0.0;
+        if (r->is_csr) {
+            for (int64_t k = 0; k < r->nnz; ++k)
+                if (r->val[k] != 0.0) margin = margin + r->val[k] * wi[r->idx[k]];
+        } else {
+            for (int32_t j = 0; j < d; ++j)
+                if (r->x[j] != 0.0) margin = margin + r->x[j] * wi[j];
+        }
+        if (i == ly) marginY = margin;
+        if (margin > maxMargin) {
+            maxMargin = margin;
+            maxMarginIndex = i;
+        }
+        margins[i] = margin;
+    }
+    double sum = 0.0;
+    if (maxMargin > 0) {
+        for (int32_t i = 0; i < C1; ++i) {
+            margins[i] = margins[i] - maxMargin;
+            if (i == maxMarginIndex) sum = sum + exp(-maxMargin);
+            else sum = sum + exp(margins[i]);
+        }
+    } else {
+        for (int32_t i = 0; i < C1; ++i) sum = sum + exp(margins[i]);
+    }
+    out->is_dense = 1;
+    memset(out->g, 0, sizeof(double) * (size_t)C1 * (size_t)d);
+    for (int32_t i = 0; i < C1; ++i) {
+        const double multiplier = exp(margins[i]) / (sum + 1.0) -
+                                  ((label != 0.0 && label == (double)(i + 1)) ? 1.0 : 0.0);
+        double* gi = out->g + (size_t)i * (size_t)d;
+        if (r->is_csr) {
+            for (int64_t k = 0; k < r->nnz; ++k)
+                if (r->val[k] != 0.0) gi[r->idx[k]] = gi[r->idx[k]] + multiplier * r->val[k];
+        } else {
+            for (int32_t j = 0; j < d; ++j)
+                if (r->x[j] != 0.0) gi[j] = gi[j] + multiplier * r->x[j];
+        }
+    }
+    const double loss = label > 0.0 ? log1p(sum) - marginY : log1p(sum);
+    return maxMargin > 0 ? loss + maxMargin : loss;
+}
+
 /* [ext] MLlib 1.6.1 Gradient.scala, binary LogisticGradient / LeastSquaresGradient /
  * HingeGradient compute(data, label, weights): (gradient, loss). */
 static double gradient_compute(int kind, const row_t* r, double label, const double* w,
@@ -269,7 +341,8 @@ double or_initial_regval(int32_t d, const double* w, const or_params* prm) {
 static int chain_rows(const or_matrix* m, int64_t r0, int64_t r1, const int32_t* rows,
                       const or_params* prm, const double* w_in, double* w_out, double* rv_out,
                       double* loss_out, int64_t* count_out) {
-    int32_t d = m->d;
+    const int32_t d = or_weight_dim(m->d, prm);   /* weights; rows have m->d features */
+    const int32_t K = prm->gradient == OR_GRAD_LOGISTIC && prm->num_classes > 2 ? prm->num_classes : 0;
     size_t nd = (size_t)(d > 0 ? d : 1);
     int64_t max_nnz = 0;
     if (m->is_csr)
@@ -278,7 +351,7 @@ static int chain_rows(const or_matrix* m, int64_t r0, int64_t r1, const int32_t*
             int64_t z = m->row_ptr[r + 1] - m->row_ptr[r];
             if (z > max_nnz) max_nnz = z;
         }
-    double* buf = (double*)malloc(sizeof(double) * (nd * 6 + (size_t)max_nnz + 1));
+    double* buf = (double*)malloc(sizeof(double) * (nd * 6 + (size_t)max_nnz + 1 + (size_t)K));
     if (!buf) return -1;
     double* w = buf;
     double* old = buf + nd;
@@ -287,6 +360,7 @@ static int chain_rows(const or_matrix* m, int64_t r0, int64_t r1, const int32_t*
     double* sa = buf + 4 * nd;
     double* sb = buf + 5 * nd;
     double* gv = buf + 6 * nd;
+    double* margins = gv + max_nnz + 1;
 
     memcpy(w, w_in, sizeof(double) * (size_t)d);   /* localWeights = bcWeights.value */
     memcpy(old, w_in, sizeof(double) * (size_t)d); /* oldWeights   = bcWeights.value */
@@ -299,7 +373,7 @@ static int chain_rows(const or_matrix* m, int64_t r0, int64_t r1, const int32_t*
     gr.gv = gv;
     row_t row;
     memset(&row, 0, sizeof(row));
-    row.d = d;
+    row.d = m->d;
     row.is_csr = m->is_csr;
     for (int64_t q = r0; q < r1; ++q) {
         const int64_t r = rows ? rows[q - r0] : q;
@@ -311,7 +385,8 @@ static int chain_rows(const or_matrix* m, int64_t r0, int64_t r1, const int32_t*
         } else {
             row.x = m->X + (size_t)r * (size_t)m->ld;
         }
-        double loss = gradient_compute(prm->gradient, &row, m->labels[r], w, &gr);
+        double loss = K ? multinomial_compute(K, &row, m->labels[r], w, &gr, margins)
+                        : gradient_compute(prm->gradient, &row, m->labels[r], w, &gr);
         localRegVal = updater_compute(prm, w, d, &gr, prm->step_size, j, &st, scratch);
         localLossSum += loss;
         count += 1;
@@ -368,7 +443,7 @@ typedef struct {
 
 static void* chain_worker(void* arg) {
     chain_job* jb = (chain_job*)arg;
-    int32_t d = jb->m->d;
+    int32_t d = or_weight_dim(jb->m->d, jb->prm);
     for (int32_t p = jb->tid; p < jb->P; p += jb->nthreads) {
         int64_t r0 = jb->offs[p], r1 = jb->offs[p + 1];
         const int32_t* rows = NULL;
@@ -428,7 +503,7 @@ int or_run(const or_matrix* m, int32_t P, const int64_t* part_offsets,
            const or_params* prm, int32_t num_iterations, const double* w0,
            double* w_out, double* loss_hist, int32_t* n_hist, int64_t* chain_counts,
            int32_t n_threads) {
-    int32_t d = m->d;
+    int32_t d = or_weight_dim(m->d, prm);
     size_t nd = (size_t)(d > 0 ? d : 1);
     *n_hist = 0;
     int64_t numExamples = 0;

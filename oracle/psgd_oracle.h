@@ -18,7 +18,8 @@
  *   updaters               SGDUpdater.scala:86-98 (Simple), :126-148 (L1), :163-181 (SquaredL2),
  *                          :199-227 (AdaGrad), :252-285 (Adam)
  *   gradients              [ext] Spark MLlib 1.6.1 mllib/optimization/Gradient.scala
- *                          (LogisticGradient binary, LeastSquaresGradient, HingeGradient),
+ *                          (LogisticGradient binary and multinomial, LeastSquaresGradient,
+ *                          HingeGradient),
  *                          with BLAS.dot/axpy/scal on netlib-java F2J ddot/daxpy/dscal
  *                          (sequential left folds, no fused multiply-add) and
  *                          MLUtils.log1pExp.
@@ -62,7 +63,12 @@ typedef struct {
     double convergence_tol;
     double adam_beta, adam_gamma, adam_eps;
     double mini_batch_fraction;   /* RDD.sample(false, f, 42 + i) per iteration (PSGD.scala:242) */
+    int32_t num_classes;          /* LogisticGradient(numClasses): <= 2 binary; > 2 multinomial,
+                                     weights are (numClasses - 1) blocks of d */
 } or_params;
+
+/* Length of the weight vector: d, or (numClasses - 1) * d for the multinomial LogisticGradient. */
+int32_t or_weight_dim(int32_t d, const or_params* prm);
 
 /* One chain (ParallelizedSGD.scala:243-270) over rows [r0, r1). */
 int or_chain(const or_matrix* m, int64_t r0, int64_t r1, const or_params* prm,

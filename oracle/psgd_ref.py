@@ -200,10 +200,68 @@ def is_converged(prev, cur, tol: float) -> bool:
     return math.sqrt(s) < tol * _jmax(_norm2(cur), 1.0)
 
 
-def gradient(kind: int, row, label: float, w):
+def _d2i(x: float) -> int:
+    """Double.toInt: NaN -> 0, saturating, truncation toward zero."""
+    if x != x:
+        return 0
+    if x >= 2147483647.0:
+        return 2147483647
+    if x <= -2147483648.0:
+        return -2147483648
+    return int(x)
+
+
+def _active(row):
+    """data.foreachActive order: (index, value) pairs."""
+    if isinstance(row, tuple):
+        return list(zip(row[0], row[1]))
+    return list(enumerate(row))
+
+
+def multinomial(row, label: float, w, num_classes: int):
+    """[ext] MLlib 1.6.1 LogisticGradient(numClasses > 2).compute(data, label, weights):
+    pivot class 0, weights in numClasses - 1 blocks of dataSize, zero values skipped, margins
+    shifted by maxMargin when it is positive -> (('dense', grad), loss)."""
+    nc1 = num_classes - 1
+    d = len(w) // nc1
+    act = _active(row)
+    ly = _d2i(label) - 1
+    margin_y, max_margin, max_idx = 0.0, -math.inf, 0
+    margins = []
+    for i in range(nc1):
+        m = 0.0
+        for j, v in act:
+            if v != 0.0:
+                m += v * w[i * d + j]
+        if i == ly:
+            margin_y = m
+        if m > max_margin:
+            max_margin, max_idx = m, i
+        margins.append(m)
+    s = 0.0
+    if max_margin > 0:
+        for i in range(nc1):
+            margins[i] -= max_margin
+            s += math.exp(-max_margin) if i == max_idx else math.exp(margins[i])
+    else:
+        for i in range(nc1):
+            s += math.exp(margins[i])
+    g = [0.0] * len(w)
+    for i in range(nc1):
+        mult = math.exp(margins[i]) / (s + 1.0) - (1.0 if (label != 0.0 and label == float(i + 1)) else 0.0)
+        for j, v in act:
+            if v != 0.0:
+                g[i * d + j] += mult * v
+    loss = math.log1p(s) - margin_y if label > 0.0 else math.log1p(s)
+    return ("dense", g), (loss + max_margin if max_margin > 0 else loss)
+
+
+def gradient(kind: int, row, label: float, w, num_classes: int = 2):
     """[ext] MLlib 1.6.1 {Logistic,LeastSquares,Hinge}Gradient.compute -> (grad, loss).
 
     grad is ('dense', list) or ('sparse', idx, vals)."""
+    if kind == GRAD_LOGISTIC and num_classes > 2:
+        return multinomial(row, label, w, num_classes)
     d = len(w)
     dotv = _dot(row, w)
     sparse = isinstance(row, tuple)
@@ -306,14 +364,14 @@ def updater(kind: int, w, g, step: float, it: int, reg: float, st: UpdaterState,
     raise ValueError(kind)
 
 
-def chain(rows, labels, grad_kind, upd_kind, step, reg, tol, w_in, **kw):
+def chain(rows, labels, grad_kind, upd_kind, step, reg, tol, w_in, num_classes=2, **kw):
     """PSGD:243-270 -> (w, regVal, lossSum, count)."""
     st = UpdaterState()
     w = list(w_in)
     old = list(w_in)
     rv, loss_sum, count, j = 0.0, 0.0, 0, 1
     for row, y in zip(rows, labels):
-        g, loss = gradient(grad_kind, row, y, w)
+        g, loss = gradient(grad_kind, row, y, w, num_classes)
         rv = updater(upd_kind, w, g, step, j, reg, st, **kw)
         loss_sum += loss
         count += 1
@@ -451,7 +509,7 @@ def bernoulli_sample(seed: int, n: int, fraction: float):
 
 
 def run(partitions, grad_kind, upd_kind, step, iters, reg, w0, tol=0.001, groups=None,
-        fraction=1.0, **kw):
+        fraction=1.0, num_classes=2, **kw):
     """PSGD:188-306, batch i = data.sample(false, fraction, 42 + i) (:242).
     partitions: list of (rows, labels).
     groups: optional list of partition-index boundaries for the two-level combine tree.
@@ -476,7 +534,7 @@ def run(partitions, grad_kind, upd_kind, step, iters, reg, w0, tol=0.001, groups
             for (rows, labels), sd in zip(partitions, seeds):
                 keep = bernoulli_sample(sd, len(labels), fraction)
                 batch_parts.append(([rows[k] for k in keep], [labels[k] for k in keep]))
-        res = [chain(rows, labels, grad_kind, upd_kind, step, reg, tol, weights, **kw)
+        res = [chain(rows, labels, grad_kind, upd_kind, step, reg, tol, weights, num_classes, **kw)
                for rows, labels in batch_parts]
         counts.append([r[3] for r in res])
         acc = None

@@ -53,6 +53,7 @@ class psgd_params(C.Structure):
         ("iteration", C.c_int32), ("step_size", C.c_double), ("reg_param", C.c_double),
         ("mini_batch_fraction", C.c_double), ("convergence_tol", C.c_double),
         ("adam_beta", C.c_double), ("adam_gamma", C.c_double), ("adam_eps", C.c_double),
+        ("num_classes", C.c_int32),
     ]
 
 

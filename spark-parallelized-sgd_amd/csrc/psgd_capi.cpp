@@ -192,6 +192,10 @@ int32_t check_compat(psgd_ctx* ctx, int32_t d, int32_t dtype, int32_t layout) {
     return PSGD_OK;
 }
 
+bool multinomial(const psgd_params* p) {
+    return p->gradient == PSGD_GRADIENT_LOGISTIC && p->num_classes > 2;
+}
+
 int32_t validate_params(const psgd_params* p) {
     if (!p) return fail(PSGD_EINVAL, "params is null");
     if (p->gradient < PSGD_GRADIENT_LOGISTIC || p->gradient > PSGD_GRADIENT_HINGE)
@@ -208,7 +212,21 @@ int32_t validate_params(const psgd_params* p) {
                  p->mini_batch_fraction);
         return fail(PSGD_EINVAL, buf);
     }
+    if (multinomial(p)) {
+        if (p->num_classes - 1 > psgd::kMultinomialMaxBlocks)
+            return fail(PSGD_EUNSUPPORTED, "LogisticGradient(numClasses = " + std::to_string(p->num_classes) +
+                                               ") exceeds the built maximum of " +
+                                               std::to_string(psgd::kMultinomialMaxBlocks + 1) + " classes");
+        if (p->compute_dtype != PSGD_F64)
+            return fail(PSGD_EUNSUPPORTED, "the multinomial LogisticGradient computes in fp64 only");
+    }
     return PSGD_OK;
+}
+
+// Length of the weight vector for rows of d features: (K - 1) * d for LogisticGradient(K > 2)
+// (MLlib 1.6.1: require(weights.size % dataSize == 0 && numClasses == weights.size / dataSize + 1)).
+int64_t weight_dim(int32_t d, const psgd_params* p) {
+    return multinomial(p) ? (int64_t)(p->num_classes - 1) * d : (int64_t)d;
 }
 
 // Allocate per-chain buffers and upload descriptors (ctx->mu held).
@@ -532,12 +550,16 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
     const Part& first = ctx->parts.begin()->second;
     const int32_t d = first.d;
     const int32_t layout = first.layout;
+    const bool mn = multinomial(params);
+    if (weight_dim(d, params) > INT32_MAX) return fail(PSGD_EINVAL, "(numClasses - 1) * d overflows");
+    const int32_t dw = (int32_t)weight_dim(d, params);   // weights (and every weight-sized buffer)
     const bool stateful = params->updater == PSGD_UPDATER_ADAGRAD || params->updater == PSGD_UPDATER_ADAM;
     const bool conv = params->convergence_tol > 0.0;
-    const bool need_state = stateful || (layout == psgd::kCsr && conv);
-    // d-vectors of status per chain (chain_general: dense [SA|SB], CSR [SA|SB|SC])
-    const int state_vectors = !need_state ? 0 : layout == psgd::kCsr ? 3 : 2;
-    rc = prepare(ctx, d, state_vectors, st);
+    const bool need_state = mn || stateful || (layout == psgd::kCsr && conv);
+    // weight-sized vectors of status per chain (chain_general: dense [SA|SB], CSR [SA|SB|SC];
+    // chain_multinomial: [SA|SB|G])
+    const int state_vectors = !need_state ? 0 : (mn || layout == psgd::kCsr) ? 3 : 2;
+    rc = prepare(ctx, dw, state_vectors, st);
     if (rc) return rc;
     int64_t n_max = 0, max_ld = 0, min_ld = INT64_MAX, max_nnz = 0;
     for (auto& kv : ctx->parts) {
@@ -631,11 +653,12 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
     kp.eps = params->adam_eps;
     kp.d = d;
     kp.n_chains = P;
+    kp.nc = mn ? params->num_classes - 1 : 0;
 
     if (sample_empty) {
         // RDD.sample with fraction 0: every partition is empty -> (w_in, 0, 0, 0) per chain.
         for (int p = 0; p < P; ++p)
-            HIP_TRY(hipMemcpyAsync(L.w_out + (size_t)p * d, d_w_in, (size_t)d * sizeof(double),
+            HIP_TRY(hipMemcpyAsync(L.w_out + (size_t)p * dw, d_w_in, (size_t)dw * sizeof(double),
                                    hipMemcpyDeviceToDevice, st));
         HIP_TRY(hipMemsetAsync(L.rv, 0, P * sizeof(double), st));
         HIP_TRY(hipMemsetAsync(L.loss, 0, P * sizeof(double), st));
@@ -670,7 +693,7 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         if (e) return fail(PSGD_EDEVICE, std::string("chain kernel launch failed: ") +
                                              hipGetErrorString((hipError_t)e));
     }
-    int e = psgd::launch_fold(L.w_out, d, L.rv, L.loss, L.cnt_d, 1, P, d, d_partial, L.watchdog, st);
+    int e = psgd::launch_fold(L.w_out, dw, L.rv, L.loss, L.cnt_d, 1, P, dw, d_partial, L.watchdog, st);
     if (e) return fail(PSGD_EDEVICE, "fold kernel launch failed");
     if (d_chain_counts)
         HIP_TRY(hipMemcpyAsync(d_chain_counts, L.cnt, (size_t)P * sizeof(int64_t),
@@ -683,12 +706,16 @@ int32_t psgd_run_epoch(psgd_ctx* ctx, const psgd_params* params, const double* w
                        int64_t* count_out, int64_t* chain_counts) {
     if (!ctx) return fail(PSGD_EINVAL, "ctx is null");
     if (!w_in || !w_out) return fail(PSGD_EINVAL, "w_in/w_out are null");
+    int32_t rc0 = validate_params(params);
+    if (rc0) return rc0;
     int32_t d = 0;
     size_t P = 0;
     {
         std::lock_guard<std::mutex> lk(ctx->mu);
         if (ctx->parts.empty()) return fail(PSGD_ESTATE, "no partitions registered");
-        d = ctx->parts.begin()->second.d;
+        const int64_t dw = weight_dim(ctx->parts.begin()->second.d, params);
+        if (dw > INT32_MAX) return fail(PSGD_EINVAL, "(numClasses - 1) * d overflows");
+        d = (int32_t)dw;   // the weight vector's length from here on
         P = ctx->parts.size();
         DeviceGuard g(ctx->device);
         HIP_TRY(ctx->w_in.ensure((size_t)d * sizeof(double)));

@@ -23,9 +23,14 @@ struct KParams {
     double reg;
     double tol;
     double beta, gamma, eps;  // AdamSGDUpdater (UPD.scala:241-244)
-    int32_t d;
+    int32_t d;                // features per row
     int32_t n_chains;
+    int32_t nc = 0;           // multinomial LogisticGradient: K - 1 weight blocks of d; 0: binary
 };
+
+// LogisticGradient(numClasses = K): at most this many weight blocks (K - 1), the chain keeps
+// the K-1 margins and multipliers in LDS (16 bytes a class).
+constexpr int kMultinomialMaxBlocks = 4096;
 
 enum Layout { kDense = 0, kCsr = 1 };
 
@@ -83,6 +88,11 @@ int csr_max_nnz(const int64_t* d_row_ptr, int64_t n, int64_t* out, hipStream_t s
 // descriptors `base`, the epoch's descriptors `out` (rows/y/n_rows of the sampled subsequence;
 // rows and labels in `rows`/`ys`, `stride` entries per chain). xs_state[c] is the chain's
 // XORShiftRandom state (hashSeed of its partition seed, computed by the host).
+// The multinomial LogisticGradient chain (psgd_multinomial.hip): fp64 compute, any updater,
+// dense or CSR rows. L.w_out holds n_chains * nc * d doubles, L.state 3 * nc * d per chain.
+int launch_multinomial_chains(const ChainLaunch& L, const KParams& kp, int layout, int storage, int updater,
+                              bool check_conv, hipStream_t stream, int* kernel_variant);
+
 int launch_sample(const ChainDesc* base, ChainDesc* out, const uint64_t* xs_state, double fraction,
                   int32_t* rows, double* ys, int64_t stride, int n_chains, hipStream_t stream);
 

@@ -692,6 +692,8 @@ int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int stora
                   int gradient, int updater, bool check_conv, int64_t min_ld, int64_t max_ld,
                   int lds_spread, hipStream_t stream, int* kernel_variant, int64_t max_nnz) {
     if (kp.n_chains <= 0) return 0;
+    if (kp.nc > 0)   // LogisticGradient(numClasses > 2)
+        return launch_multinomial_chains(L, kp, layout, storage, updater, check_conv, stream, kernel_variant);
     // PSGD_PER_SAMPLE=1 keeps fp32 mode on the per-sample kernel (A/B measurements)
     static const bool per_sample = [] {
         const char* e = getenv("PSGD_PER_SAMPLE");

@@ -21,8 +21,14 @@ class Gradient:
 
 
 class LogisticGradient(Gradient):
-    """Binary logistic loss: margin = -dot(x, w); mult = 1/(1+exp(margin)) - y;
-    grad = mult * x; loss = y > 0 ? log1pExp(margin) : log1pExp(margin) - margin."""
+    """numClasses = 2 (binary): margin = -dot(x, w); mult = 1/(1+exp(margin)) - y;
+    grad = mult * x; loss = y > 0 ? log1pExp(margin) : log1pExp(margin) - margin.
+
+    numClasses = K > 2 (multinomial, class 0 the pivot): weights are K - 1 blocks of d;
+    margin_i = x . w_i over x's non-zero values; with M = max margin shifted out when positive,
+    mult_i = exp(margin_i) / (sum + 1) - [y == i + 1]; grad block i = mult_i * x;
+    loss = log1p(sum) - margin_y (y > 0) (+ M when positive). Computed in fp64
+    (chain_multinomial, csrc/psgd_multinomial.hip)."""
 
     kind = 0
 
@@ -30,10 +36,7 @@ class LogisticGradient(Gradient):
         if numClasses < 2:
             raise IllegalArgumentException(
                 f"requirement failed: numClasses must be >= 2 but got {numClasses}")
-        if numClasses != 2:
-            raise UnsupportedOperationException(
-                "multinomial LogisticGradient(numClasses > 2) is not built (SURVEY §8f rank 4)")
-        self.numClasses = numClasses
+        self.numClasses = int(numClasses)
 
     def __repr__(self) -> str:
         return f"LogisticGradient(numClasses={self.numClasses})"
@@ -49,6 +52,17 @@ class HingeGradient(Gradient):
     """ls = 2y - 1; if 1 > ls * dot(x, w): grad = -ls * x, loss = 1 - ls * dot; else 0, 0."""
 
     kind = 2
+
+
+def num_classes(g) -> int:
+    """numClasses of a LogisticGradient (2 for every other gradient)."""
+    return int(getattr(g, "numClasses", 2)) if isinstance(g, LogisticGradient) else 2
+
+
+def weight_dim(g, num_features: int) -> int:
+    """Length of the weight vector the gradient expects for rows of num_features."""
+    k = num_classes(g)
+    return (k - 1) * num_features if k > 2 else num_features
 
 
 def gradient_kind(g) -> int:

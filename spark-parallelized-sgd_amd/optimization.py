@@ -26,7 +26,7 @@ import numpy as np
 from . import _native as N
 from .data import (CsrPartition, DensePartition, DeviceCsrPartition, DevicePartition, PartitionedData,
                    shard_range)
-from .gradient import Gradient, gradient_kind
+from .gradient import Gradient, LogisticGradient, gradient_kind, num_classes, weight_dim
 from .updater import AdamSGDUpdater, SGDUpdater, updater_kind
 
 log = logging.getLogger("org.apache.spark.mllib.optimization.ParallelizedSGD")
@@ -50,6 +50,7 @@ def make_params(gradient, updater, stepSize, regParam, miniBatchFraction, conver
                 compute_dtype="f64", iteration=1) -> N.psgd_params:
     p = N.psgd_params()
     p.gradient = gradient_kind(gradient)
+    p.num_classes = num_classes(gradient)
     p.updater = updater_kind(updater)
     p.compute_dtype = {"f64": N.F64, "f32": N.F32}[compute_dtype]
     p.iteration = iteration
@@ -100,8 +101,9 @@ class ShardedEngine:
     partitions contributes the fold's identity element (w_in, 0, 0, 0): an empty partition's
     result (ParallelizedSGD.scala:270 with count 0)."""
 
-    def __init__(self, data: PartitionedData, rank: int, world: int):
-        self.d = data.num_features
+    def __init__(self, data: PartitionedData, rank: int, world: int, weight_dim: Optional[int] = None):
+        # length of the weight vector: num_features, (K-1)*num_features for multinomial Logistic
+        self.d = int(weight_dim) if weight_dim else data.num_features
         self.rank, self.world = rank, world
         self.lo, self.hi = shard_range(data.num_partitions, rank, world)
         self.n_local = self.hi - self.lo
@@ -135,11 +137,11 @@ class HipEngine(ShardedEngine):
     `self.stream`."""
 
     def __init__(self, data: PartitionedData, rank: int = 0, world: int = 1,
-                 device: Optional[int] = None):
+                 device: Optional[int] = None, weight_dim: Optional[int] = None):
         import torch
         if not torch.cuda.is_available():
             raise N.DeviceError("HipEngine needs a visible MI355X (torch.cuda.is_available() is False)")
-        super().__init__(data, rank, world)
+        super().__init__(data, rank, world, weight_dim)
         if device is None:
             device = torch.cuda.current_device()
         self.torch = torch
@@ -328,14 +330,20 @@ class ParallelizedSGD:
             return out + (chain_counts,) if return_chain_counts else out
         if numExamples * miniBatchFraction < 1:  # :219-221
             log.warning("The miniBatchFraction is too small")
-        if w0.shape[0] != data.num_features:
+        nf = data.num_features
+        if isinstance(gradient, LogisticGradient):
+            # LogisticGradient.compute: require(weights.size % dataSize == 0 &&
+            # numClasses == weights.size / dataSize + 1) [ext MLlib 1.6.1]
+            if nf == 0 or w0.shape[0] % nf != 0 or num_classes(gradient) != w0.shape[0] // nf + 1:
+                raise IllegalArgumentException("requirement failed")
+        elif w0.shape[0] != nf:
             raise IllegalArgumentException(
                 f"requirement failed: BLAS.dot(x: Vector, y: Vector) was given Vectors with "
-                f"non-matching sizes: x.size = {data.num_features}, y.size = {w0.shape[0]}")
+                f"non-matching sizes: x.size = {nf}, y.size = {w0.shape[0]}")
 
         if engine is None:
             rank, world, _ = _dist()
-            engine = HipEngine(data, rank, world)
+            engine = HipEngine(data, rank, world, weight_dim=weight_dim(gradient, nf))
 
         params = make_params(gradient, updater, stepSize, regParam, miniBatchFraction,
                              convergenceTol, compute_dtype)

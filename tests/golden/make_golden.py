@@ -47,11 +47,13 @@ def py_partitions_csr(rp, col, val, y, offs):
 
 def run_both(case, mat, py_parts, offs):
     frac = case.get("fraction", 1.0)
-    kw = dict(tol=case["tol"], fraction=frac)
+    nc = case.get("num_classes", 2)
+    kw = dict(tol=case["tol"], fraction=frac, num_classes=nc)
     w, h, c = O.run(mat, offs, case["gradient"], case["updater"], case["step"], case["iters"],
                     case["reg"], np.array(case["w0"]), **kw)
     wp, hp, cp = R.run(py_parts, GRAD[case["gradient"]], UPD[case["updater"]], case["step"],
-                       case["iters"], case["reg"], list(case["w0"]), tol=case["tol"], fraction=frac)
+                       case["iters"], case["reg"], list(case["w0"]), tol=case["tol"], fraction=frac,
+                       num_classes=nc)
     same = lambda a, b: len(a) == len(b) and all(x == y or (x != x and y != y) for x, y in zip(a, b))
     assert same(list(map(float, w)), wp), (case["name"], "weights differ between C and Python")
     assert same(list(map(float, h)), hp), (case["name"], "loss history differs")
@@ -192,6 +194,47 @@ def main():
                  w0=[0.0] * d, row_ptr=rp.tolist(), col=col.tolist(), val=val.tolist(), y=yr.tolist())
         mat = O.Matrix(yr, row_ptr=rp, col=col, val=val, d=d)
         cases.append(run_both(c, mat, py_partitions_csr(rp, col, val, yr, offs), offs))
+
+    # --- multinomial LogisticGradient(numClasses > 2) [ext MLlib 1.6.1]: weights (K-1)*d ---
+    for K, u, tol, layout in ((3, "simple", 0.0, "dense"), (3, "squared_l2", 0.01, "dense"),
+                              (5, "l1", 0.0, "dense"), (4, "adagrad", 0.0, "dense"),
+                              (3, "adam", 0.01, "dense"), (6, "simple", 0.0, "csr"),
+                              (3, "squared_l2", 0.0, "csr"), (4, "adagrad", 0.01, "csr"),
+                              (5, "adam", 0.0, "csr"), (3, "l1", 0.01, "csr")):
+        n, d = 180, 7 if layout == "dense" else 30
+        W = rng.standard_normal((K, d))
+        # labels 0..K-1, a few out of range (K) and a non-integer one: the reference accepts them
+        if layout == "dense":
+            Xr = rng.standard_normal((n, d)).round(6)
+            Xr[rng.uniform(size=(n, d)) < 0.15] = 0.0   # zero values are skipped by foreachActive
+            logits = Xr @ W.T
+        else:
+            rp, col, val = [0], [], []
+            for r in range(n):
+                k = int(rng.integers(0, 9))
+                col += sorted(rng.choice(d, size=k, replace=False).tolist())
+                val += list(map(float, rng.uniform(-1, 1, size=k).round(6)))
+                rp.append(len(col))
+            rp, col, val = np.array(rp), np.array(col, np.int32), np.array(val)
+            dense = np.zeros((n, d))
+            for r in range(n):
+                dense[r, col[rp[r]:rp[r + 1]]] = val[rp[r]:rp[r + 1]]
+            logits = dense @ W.T
+        yr = np.argmax(logits + rng.gumbel(size=logits.shape), 1).astype(float)
+        yr[:3] = [float(K), 1.5, -1.0]
+        offs = [0, 60, 61, 180]
+        w0 = list(map(float, (0.5 * rng.standard_normal((K - 1) * d)).round(6)))
+        step = 0.3
+        c = dict(name=f"multinomial_k{K}_{layout}_{u}_tol{tol}", source="random", n=n, d=d, offsets=offs,
+                 gradient="logistic", num_classes=K, updater=u, step=step, iters=3, reg=0.01, tol=tol,
+                 w0=w0, y=yr.tolist())
+        if layout == "dense":
+            c["X"] = Xr.tolist()
+            cases.append(run_both(c, O.Matrix(yr, Xr), py_partitions_dense(Xr, yr, offs), offs))
+        else:
+            c.update(row_ptr=rp.tolist(), col=col.tolist(), val=val.tolist())
+            mat = O.Matrix(yr, row_ptr=rp, col=col, val=val, d=d)
+            cases.append(run_both(c, mat, py_partitions_csr(rp, col, val, yr, offs), offs))
 
     out = os.path.join(HERE, "golden_cases.json")
     with open(out, "w") as f:

@@ -64,8 +64,25 @@ def test_unsupported_plugins_raise(pkg):
 
     with pytest.raises(pkg.IllegalArgumentException):
         pkg.make_params(MyGradient(), pkg.SimpleSGDUpdater(), 1.0, 0.0, 1.0, 0.0)
-    with pytest.raises(pkg.UnsupportedOperationException):
-        pkg.LogisticGradient(numClasses=3)
+    with pytest.raises(pkg.IllegalArgumentException):
+        pkg.LogisticGradient(numClasses=1)
+
+
+def test_multinomial_params_and_weight_size(pkg):
+    """LogisticGradient(numClasses = K): params carry K, and the weight vector must be (K-1)*d
+    (MLlib's require(weights.size % dataSize == 0 && numClasses == weights.size / dataSize + 1))."""
+    g = pkg.LogisticGradient(numClasses=4)
+    p = pkg.make_params(g, pkg.SimpleSGDUpdater(), 1.0, 0.0, 1.0, 0.0)
+    assert p.num_classes == 4 and p.gradient == 0
+    assert pkg.make_params(pkg.HingeGradient(), pkg.SimpleSGDUpdater(), 1.0, 0.0, 1.0, 0.0).num_classes == 2
+    X = np.ones((4, 3))
+    data = pkg.PartitionedData([pkg.DensePartition(np.zeros(4), X)])
+    for bad in (3, 7, 12):   # (K-1)*d = 9
+        with pytest.raises(pkg.IllegalArgumentException, match="requirement failed"):
+            pkg.runParallelizedSGD(data, g, pkg.SimpleSGDUpdater(), 1.0, 1, 0.0, 1.0, np.zeros(bad), 0.0)
+    with pytest.raises(pkg.IllegalArgumentException, match="requirement failed"):
+        pkg.runParallelizedSGD(data, pkg.LogisticGradient(), pkg.SimpleSGDUpdater(), 1.0, 1, 0.0, 1.0,
+                               np.zeros(9), 0.0)
 
 
 class ScriptedEngine:

@@ -63,7 +63,7 @@ def data_for(pkg, oracle, case):
 
 
 def run_case(pkg, data, case, **kw):
-    g = getattr(pkg, G[case["gradient"]])()
+    g = getattr(pkg, G[case["gradient"]])(*([case["num_classes"]] if "num_classes" in case else []))
     u = getattr(pkg, U[case["updater"]])()
     return pkg.runParallelizedSGD(data, g, u, case["step"], case["iters"], case["reg"],
                                   case.get("fraction", 1.0), np.array(case["w0"]), case["tol"],

@@ -134,7 +134,7 @@ def test_golden_fixtures_reproduce(oracle, golden):
                               col=np.array(case["col"]), val=np.array(case["val"]), d=case["d"])
         w, h, c = oracle.run(m, case["offsets"], case["gradient"], case["updater"], case["step"],
                              case["iters"], case["reg"], np.array(case["w0"]), tol=case["tol"],
-                             fraction=case.get("fraction", 1.0))
+                             fraction=case.get("fraction", 1.0), num_classes=case.get("num_classes", 2))
         e = case["expected"]
         assert list(map(float, w)) == e["weights"], case["name"]
         assert list(map(float, h)) == e["loss_history"], case["name"]
@@ -170,3 +170,36 @@ def test_sampler_c_and_python_agree(oracle):
     for f in (0.1, 0.7):
         m = sum(len(oracle.sample_partition(int(sd), 20000, f)) for sd in oracle.partition_seeds(46, 5))
         assert abs(m / 100000 - f) < 0.01
+
+
+def test_multinomial_gradient_is_softmax_cross_entropy():
+    """The multinomial LogisticGradient restatement (C and Python) against the textbook form:
+    loss = logsumexp([0, m_1..m_{K-1}]) - m_y, gradient block i = (p_{i+1} - [y == i+1]) x,
+    in both regimes of the reference's max-margin shift (M > 0 and M <= 0) -- a property check
+    independent of the reference's evaluation order."""
+    import psgd_ref as R
+    rng = np.random.default_rng(5)
+    for K, scale in ((3, 0.1), (5, 3.0), (7, 0.5)):
+        d = 6
+        for _ in range(20):
+            x = rng.standard_normal(d)
+            x[rng.uniform(size=d) < 0.2] = 0.0
+            w = scale * rng.standard_normal((K - 1) * d)
+            y = float(rng.integers(0, K))
+            (_, g), loss = R.multinomial(list(x), y, list(w), K)
+            m = np.concatenate([[0.0], w.reshape(K - 1, d) @ x])
+            lse = np.log(np.sum(np.exp(m - m.max()))) + m.max()
+            assert abs(loss - (lse - m[int(y)])) <= 1e-12 * max(1.0, abs(loss))
+            p = np.exp(m - lse)
+            want = np.concatenate([(p[i + 1] - (1.0 if y == i + 1 else 0.0)) * x for i in range(K - 1)])
+            assert np.allclose(g, want, rtol=1e-12, atol=1e-15)
+    # the C restatement agrees with the Python one bit for bit on a one-sample chain
+    X = rng.standard_normal((1, 4))
+    w0 = rng.standard_normal(12)
+    for lab in (0.0, 2.0, 3.0, 4.0, 1.5):
+        import oracle as O
+        mat = O.Matrix(np.array([lab]), X)
+        w, h, _ = O.run(mat, [0, 1], "logistic", "simple", 1.0, 1, 0.0, w0, tol=0.0, num_classes=4)
+        wp, hp, _ = R.run([([list(X[0])], [lab])], R.GRAD_LOGISTIC, R.UPD_SIMPLE, 1.0, 1, 0.0, list(w0),
+                          tol=0.0, num_classes=4)
+        assert list(map(float, w)) == wp and list(map(float, h)) == hp
