@@ -294,6 +294,14 @@ __global__ __launch_bounds__(64) void chain_general(ChainLaunch L, KParams kp) {
         for (int i = lane; i < d; i += 64) SC[i] = 0.0;
     wave_mem_fence();
 
+    // CSR rows with SquaredL2 and no per-sample convergence test: the alpha-scaled lazy form
+    // (SURVEY §8a a7). The chain keeps w = alpha * v, so the reference's O(d) scale
+    // w *= 1 - s*lambda (UPD.scala:169) is one multiply of alpha and the gradient step adds
+    // (-s g_j) / alpha to v_j at the row's indices; alpha is folded back into v (O(d)) when it
+    // leaves [2^-400, 2^400] or becomes 0, and at the chain's end. Equal to the reference's
+    // arithmetic up to rounding (the 1e-9 fp64 bar).
+    constexpr bool LAZY = LAYOUT == kCsr && UPD == U_SQUARED_L2 && !CONV;
+    double alpha = 1.0;
     double loss_sum = 0.0;
     int64_t count = 0;
     double rv = 0.0;
@@ -314,7 +322,8 @@ __global__ __launch_bounds__(64) void chain_general(ChainLaunch L, KParams kp) {
             for (int64_t k = kb + lane; k < ke; k += 64)
                 acc = m_fma(double(X[k]), W[COL[k]], acc);
         }
-        const double z = wave_sum(acc);
+        double z = wave_sum(acc);
+        if constexpr (LAZY) z = alpha * z;   // dot(x, w) with w = alpha * v
         double mult;
         const double loss = gradient_scalar<GRAD, double>(z, y, mult);
         loss_sum += loss;
@@ -340,7 +349,21 @@ __global__ __launch_bounds__(64) void chain_general(ChainLaunch L, KParams kp) {
                 // Updaters that touch every coordinate: run the elementwise part over all d,
                 // with the gradient applied at the row's indices in a second pass (ordered as
                 // the reference: L2 scales before the axpy, L1 thresholds after it).
-                if constexpr (UPD == U_SQUARED_L2) {
+                if constexpr (LAZY) {
+                    const double c = 1.0 - s * kp.reg;
+                    const double na = alpha * c;
+                    if (!(__builtin_fabs(na) >= 0x1p-400 && __builtin_fabs(na) <= 0x1p400)) {
+                        for (int i = lane; i < d; i += 64) W[i] = (alpha * W[i]) * c;
+                        alpha = 1.0;
+                        wave_mem_fence();
+                    } else {
+                        alpha = na;
+                    }
+                    for (int64_t k = kb + lane; k < ke; k += 64) {
+                        const int i = COL[k];
+                        W[i] = W[i] + (a * (mult * double(X[k]))) / alpha;
+                    }
+                } else if constexpr (UPD == U_SQUARED_L2) {
                     const double c = 1.0 - s * kp.reg;
                     for (int i = lane; i < d; i += 64) {
                         const double old = W[i];
@@ -492,6 +515,10 @@ __global__ __launch_bounds__(64) void chain_general(ChainLaunch L, KParams kp) {
         }
     }
 
+    if constexpr (LAZY) {
+        for (int i = lane; i < d; i += 64) W[i] = alpha * W[i];
+        wave_mem_fence();
+    }
     if constexpr (UPD == U_SQUARED_L2 || UPD == U_L1) {
         double acc = 0.0;
         for (int i = lane; i < d; i += 64) acc += (UPD == U_SQUARED_L2) ? W[i] * W[i] : fabs(W[i]);

@@ -216,6 +216,38 @@ def test_csr_stateful_updater(pkg, oracle):
         assert_close(h, hr, what=upd + " loss")
 
 
+@pytest.mark.parametrize("reg,step", [(0.01, 0.5), (0.999, 1.0), (1.0, 1.0), (3.0, 1.0), (1e-6, 0.5)])
+def test_csr_squared_l2_alpha_scaled(pkg, oracle, reg, step):
+    """fp64 CSR SquaredL2 without a convergence test keeps w = alpha * v (O(nnz) per sample):
+    against the oracle's O(d) scale per sample at the 1e-9 bar, including alpha leaving
+    [2^-400, 2^400] (folded back into v), 1 - s*lambda == 0 exactly (reg 1, step 1 at j = 1)
+    and negative factors (reg 3)."""
+    rng = np.random.default_rng(int(reg * 1000) + 7)
+    n, d = 1200, 5000
+    rp, col, val = [0], [], []
+    for _ in range(n):
+        k = int(rng.integers(0, 40))
+        col += sorted(rng.choice(d, size=k, replace=False).tolist())
+        val += rng.uniform(0, 1, size=k).tolist()
+        rp.append(len(col))
+    rp, col, val = np.array(rp), np.array(col, np.int32), np.array(val)
+    y = (rng.uniform(size=n) > 0.5).astype(float)
+    offs = [0, 500, 500, 1200]
+    parts = [pkg.CsrPartition(y[a:b], rp[a:b + 1] - rp[a], col[rp[a]:rp[b]], val[rp[a]:rp[b]], d)
+             for a, b in zip(offs[:-1], offs[1:])]
+    w0 = 0.1 * rng.standard_normal(d)
+    for grad in ("logistic", "hinge"):
+        w, h, counts = pkg.runParallelizedSGD(pkg.PartitionedData(parts), getattr(pkg, G[grad])(),
+                                              pkg.SquaredL2SGDUpdater(), step, 3, reg, 1.0, w0, 0.0,
+                                              return_chain_counts=True)
+        assert pkg.optimization.get_context(0).last_kernel() == 201
+        wr, hr, cr = oracle.run(oracle.Matrix(y, row_ptr=rp, col=col, val=val, d=d), offs, grad, "squared_l2",
+                                step, 3, reg, w0, tol=0.0)
+        assert [list(map(int, c)) for c in counts] == [list(map(int, c)) for c in cr]
+        assert_close(w, wr, what=f"{grad} reg={reg} weights")
+        assert_close(h, hr, what=f"{grad} reg={reg} loss")
+
+
 def test_mini_batch_fraction(pkg, oracle):
     """miniBatchFraction < 1: batch i = data.sample(false, f, 42 + i) (PSGD.scala:242) through
     the fp32 block kernel and the per-sample kernels (the fp64 path is in the golden cases);
