@@ -346,6 +346,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             __hip_atomic_store(&hdr->consumed, (unsigned)(t0 + kk), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
         }
+        // The flags this block will test, read now: one wave per SIMD hides no LDS latency, so a
+        // flag read where it is tested costs a full LDS round trip per block (~30 cycles per row
+        // at c2); read here it lands under the dots. (Relaxed: LDS accesses of a workgroup are
+        // performed in order, and the data they guard is read only after the test.)
+        const unsigned gpre = __hip_atomic_load(&ghdr->gdone[b & 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const unsigned rpre = __hip_atomic_load(&hdr->ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         // p_k = x_k . W (one packed accumulator per row; eight rows interleave)
         PSGD_STAMP(const uint64_t st_a = __builtin_amdgcn_s_memtime();)
         float pk[kBlk];
@@ -385,7 +391,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         {
             const unsigned need = (unsigned)(b >> 1) + 1;
             unsigned* gd = &ghdr->gdone[b & 1];
-            if (__hip_atomic_load(gd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+            if (gpre < need) {
                 const uint64_t tw = __builtin_amdgcn_s_memrealtime();
                 while (__hip_atomic_load(gd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
                     if (__builtin_amdgcn_s_memrealtime() - tw > kWatchdogTicks) {
@@ -430,6 +436,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             if ((b & 3) == 3) { loss_sum += double(loss_blk); loss_blk = 0.0f; }
         }
         count += kk;
+        if (rpre > ready) ready = rpre;   // the next block's wait_rows rarely reads the flag again
 
         // W <- a_i W + c_i x_i, i = 0..kk-1, in sample order
 #pragma unroll

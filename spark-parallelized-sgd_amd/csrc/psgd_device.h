@@ -323,6 +323,7 @@ __device__ __forceinline__ void ring_loader(const ChainLaunch& L, const ChainDes
     const unsigned* msrc = reinterpret_cast<const unsigned*>((lane & 2) ? L.steps : dsc.y) + (lane & 1);
     const int mrow = lane >> 2;
     int64_t limit = R;            // rows < limit have a free slot
+    int64_t pub = 0;              // rows published in hdr->ready (never decreases)
     int slot = 0, mslot = 0;
     // sampled epoch: sample t is row rows[t], read with scalar loads (constant address space)
     const int32_t __attribute__((address_space(4)))* RIDX =
@@ -355,7 +356,10 @@ __device__ __forceinline__ void ring_loader(const ChainLaunch& L, const ChainDes
             if (R < D + 2 * PUB + 2 * GB) {
                 asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
                 lds_store_u32_nowait(&hdr->ready, (unsigned)t);
+                pub = t;
             }
+            // rows issued but not published yet (the youngest D: see the publish below)
+            int inflight = (int)(t - pub);
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             for (;;) {
                 unsigned c = __builtin_amdgcn_readfirstlane(lds_load_u32_asm(&hdr->consumed));
@@ -368,6 +372,16 @@ __device__ __forceinline__ void ring_loader(const ChainLaunch& L, const ChainDes
                 }
                 limit = (int64_t)c + R;
                 if (te <= limit) break;
+                if (inflight > 0) {
+                    // while the ring is full, publish the in-flight rows as they land (PUB at a
+                    // time) rather than only after the next group: the consumers see the whole
+                    // ring, not R - D rows of it
+                    inflight = inflight > PUB ? inflight - PUB : 0;
+                    wait_vmcnt_le(inflight * NV);
+                    pub = t - inflight;
+                    lds_store_u32_nowait(&hdr->ready, (unsigned)pub);
+                    continue;
+                }
                 if (__builtin_amdgcn_readfirstlane(lds_load_u32_asm(&hdr->stop))) goto drain;
                 if (__builtin_amdgcn_s_memrealtime() - t0 > kWatchdogTicks) {
                     __hip_atomic_fetch_or(L.watchdog, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -402,7 +416,10 @@ __device__ __forceinline__ void ring_loader(const ChainLaunch& L, const ChainDes
             PSGD_STAMP(const uint64_t st_v = __builtin_amdgcn_s_memtime();)
             wait_vmcnt_le(D * NV);
             PSGD_STAMP(st_vm += __builtin_amdgcn_s_memtime() - st_v;)
-            lds_store_u32_nowait(&hdr->ready, (unsigned)(te - D));
+            if (te - D > pub) {
+                pub = te - D;
+                lds_store_u32_nowait(&hdr->ready, (unsigned)pub);
+            }
         }
     }
 drain:
