@@ -42,7 +42,7 @@ static_assert(kMetaRows == 2 * kBlk, "a meta block holds two row blocks");
 
 struct GramHeader {
     unsigned gdone[2];   // blocks finished by Gram wave 0 (even blocks) / 1 (odd blocks)
-    unsigned pad[2];
+    unsigned gread[2];   // blocks whose rows Gram wave 0 / 1 holds in registers (ring slots free)
 };
 
 // --- transposed wave reductions -----------------------------------------------------------
@@ -175,13 +175,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         hdr->stop = 0;
         ghdr->gdone[0] = 0;
         ghdr->gdone[1] = 0;
+        ghdr->gread[0] = 0;
+        ghdr->gread[1] = 0;
     }
     // entries on and above the diagonal stay zero (the Gram waves write only i < k)
     for (int i = threadIdx.x; i < GS * kBlk * kBlk; i += blockDim.x) gring[i] = 0.0f;
     __syncthreads();
 
     if (wave == 1) {
-        ring_loader<S, NV, FULL, kBlk, kBlk>(L, dsc, hdr, meta_ring, ring, geom, lane, ghdr->gdone);
+        ring_loader<S, NV, FULL, kBlk, kBlk>(L, dsc, hdr, meta_ring, ring, geom, lane, ghdr->gread);
         return;
     }
 
@@ -244,14 +246,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             const char* base = ring + rs * ROW_BYTES;
             rs += 2 * kBlk;
             if (rs >= R) rs -= R;
+            // NV >= 4: the whole block into registers first, then hand its ring slots back: the
+            // loader refills them while the pair dots run (with a 4-block ring at d = 1,024 the
+            // slots held for the Gram's ~2,000 cycles are what the row stream waits for; c3
+            // 3-5 % faster). At NV = 2 (9-block ring) the early hand-back measured 1-2 % slower.
+            constexpr bool EARLY = NV >= 4;
+            T2 xall[NV][kBlk][H];
+#pragma unroll
+            for (int v = 0; v < NV; ++v)
+#pragma unroll
+                for (int k = 0; k < kBlk; ++k) to_pairs(read_vec(base + k * ROW_BYTES, v), xall[v][k]);
+            if constexpr (EARLY) {
+                asm volatile("s_waitcnt lgkmcnt(0)" : : : "memory");
+                __hip_atomic_store(&ghdr->gread[gw], done + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
             T2 acc[kPairs];
 #pragma unroll
             for (int q = 0; q < kPairs; ++q) acc[q] = T2{0.0f, 0.0f};
 #pragma unroll
             for (int v = 0; v < NV; ++v) {
-                T2 xc[kBlk][H];
-#pragma unroll
-                for (int k = 0; k < kBlk; ++k) to_pairs(read_vec(base + k * ROW_BYTES, v), xc[k]);
+                auto& xc = xall[v];
                 int q = 0;
 #pragma unroll
                 for (int k = 1; k < kBlk; ++k)
@@ -274,6 +288,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             if (goff >= 0) slot[goff] = val;
             ++done;
             __hip_atomic_store(&ghdr->gdone[gw], done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if constexpr (!EARLY)
+                __hip_atomic_store(&ghdr->gread[gw], done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         PSGD_STAMP(if (L.stamps && lane == 0) {
             unsigned long long* o = L.stamps + (size_t)chain * 16 + 8 + 4 * gw;
