@@ -200,7 +200,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                 __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 return false;
             }
-            __builtin_amdgcn_s_sleep(1);
+            if (code != 2) __builtin_amdgcn_s_sleep(1);   // the chain wave polls without sleeping
         }
     };
     // One 16-byte vector of a row slot, zero past the row end (those LDS bytes are stale).
@@ -415,7 +415,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                         __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         return false;
                     }
-                    __builtin_amdgcn_s_sleep(1);
                 }
             }
         }
