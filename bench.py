@@ -260,12 +260,25 @@ def main():
     # below steady-state clocks (rocprof trace: 3.5-3.8 ms for the first c2 epochs, 3.1 ms from
     # the sixth on), so untimed epochs run for --prewarm-s seconds before the W warmup steps.
     # The model they produce is discarded: the warmup and timed steps start from w = 0.
+    # Every epoch holds a collective when N > 1, so all ranks run the same count: two epochs
+    # time one, and the count for --prewarm-s is the max over ranks.
     w0 = w
     prewarm_epochs = 0
     if args.prewarm_s > 0:
-        t_pw = time.perf_counter()
         wp = w0
-        while time.perf_counter() - t_pw < args.prewarm_s:
+        torch.cuda.synchronize()
+        t_pw = time.perf_counter()
+        for _ in range(2):
+            wp, _, _ = one_step(wp, prewarm_epochs + 1)
+            prewarm_epochs += 1
+        torch.cuda.synchronize()
+        per_epoch = (time.perf_counter() - t_pw) / 2
+        want = max(2, min(5000, int(args.prewarm_s / max(per_epoch, 1e-6))))
+        if world > 1:
+            t = torch.tensor([want], dtype=torch.int64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            want = int(t.item())
+        while prewarm_epochs < want:
             wp, _, _ = one_step(wp, prewarm_epochs + 1)
             prewarm_epochs += 1
         torch.cuda.synchronize()
