@@ -23,6 +23,10 @@ sys.path.insert(0, ROOT)
 
 WORKLOADS = {
     # name: (gradient, rows per GPU, d, chains per GPU, step, storage dtype, BASELINE config)
+    # c1 is the reference's own CPU-runnable case (4 chains: latency-bound on a GPU, a parity
+    # config); run it with --compute f64, its precision
+    "c1": ("logistic", 100_000, 100, 4, 1.0, "f64",
+           "Logistic regression, synthetic dense 100k x 100 fp64, 4 partitions (Spark local[4] case)"),
     "c2": ("least_squares", 10_000_000, 512, 256, 1e-3, "f32",
            "Least-squares linear regression, dense 10M x 512 fp32, 256 chains on 1 MI355X"),
     "c3": ("logistic", 12_500_000, 1024, 256, 1.0, "f32",

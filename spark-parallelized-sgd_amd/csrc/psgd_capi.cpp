@@ -627,6 +627,7 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         L.stamps = ctx->stamps.as<unsigned long long>();
     }
     L.zbuf = nullptr;
+    L.zbuf64 = nullptr;
     L.zstride = 0;
     L.wf32 = nullptr;
     L.wstride = 0;
@@ -643,6 +644,13 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         L.zstride = std::max<int64_t>(n_max, 1);
         HIP_TRY(ctx->zbuf.ensure((size_t)P * (size_t)L.zstride * sizeof(float)));
         L.zbuf = ctx->zbuf.as<float>();
+    }
+    if (params->gradient == PSGD_GRADIENT_LOGISTIC && params->compute_dtype == PSGD_F64 &&
+        layout == psgd::kDense && !mn) {
+        // per-row dots of the fp64 per-sample kernel (its loss is summed after the chain)
+        L.zstride = std::max<int64_t>(n_max, 1);
+        HIP_TRY(ctx->zbuf.ensure((size_t)P * (size_t)L.zstride * sizeof(double)));
+        L.zbuf64 = ctx->zbuf.as<double>();
     }
     HIP_TRY(hipMemsetAsync(L.watchdog, 0, 16, st));
     psgd::KParams kp;

@@ -49,6 +49,7 @@ struct ChainLaunch {
     int* watchdog;           // set by a wave whose partner stopped making progress
     unsigned long long* stamps;  // per-wave cycle counters, diagnostic builds only (PSGD_STAMPS)
     float* zbuf;             // [n_chains * zstride] per-row margins (fp32 Logistic block kernel)
+    double* zbuf64;          // [n_chains * zstride] per-row dots (fp64 Logistic chain_dense)
     int64_t zstride;
     float* wf32;             // [n_chains * wstride] fp32 working weights (CSR fp32 kernel)
     int64_t wstride;

@@ -125,6 +125,9 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, Ri
 
     double loss_sum = 0.0;
     T loss_blk = T(0);          // fp32 mode: block partial, flushed to the fp64 sum every 32 rows
+    // fp64 Logistic: the per-row dots go to L.zbuf64, the losses are summed after the chain
+    constexpr bool ZEXT = GRAD == G_LOGISTIC && sizeof(T) == 8;
+    double* zout = ZEXT ? L.zbuf64 + (int64_t)chain * L.zstride : nullptr;
     int64_t count = 0;
     const char* slot_ptr = ring;                       // slot of row t
     const char* const ring_end = ring + R * ROW_BYTES;
@@ -157,7 +160,13 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, Ri
         }
 
         T mult, loss;
-        if constexpr (GRAD == G_LEAST_SQUARES) {
+        if constexpr (ZEXT) {
+            // mult as gradient_scalar; the row's loss (log1pExp: a second exp and a log1p on
+            // the sequential wave) is summed after the chain by logistic_loss64_kernel from z
+            mult = (T(1) / (T(1) + m_exp(-z))) - y;
+            loss = T(0);
+            if (lane == 0) zout[t] = z;
+        } else if constexpr (GRAD == G_LEAST_SQUARES) {
             // loss = diff*diff/2.0: the halving is exact, so the chain accumulates diff*diff and
             // halves the sum (identical to summing the halves)
             mult = z - y;
@@ -254,7 +263,7 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, Ri
     }
     if (lane == 0) {
         L.rv[chain] = rv;
-        L.loss[chain] = loss_sum;
+        if constexpr (!ZEXT) L.loss[chain] = loss_sum;
         L.cnt[chain] = count;
         L.cnt_d[chain] = double(count);
     }
@@ -601,6 +610,32 @@ __global__ __launch_bounds__(256) void sq_terms_kernel(const double* __restrict_
     if (threadIdx.x == 0) { out[0] = s0[0]; out[1] = s1[0]; }
 }
 
+// The fp64 Logistic chain's lossSum (PSGD.scala:254/:259; [ext] MLlib 1.6.1 LogisticGradient:
+// margin = -z, loss = y > 0 ? log1pExp(margin) : log1pExp(margin) - margin) from the dots z_t
+// chain_dense stored, one 1024-thread workgroup per chain. Every row's loss is the reference's
+// arithmetic on the chain's own z_t; only the sum is a tree instead of the sequential `+=`
+// (within the fp64 1e-9 bar).
+__global__ __launch_bounds__(1024) void logistic_loss64_kernel(ChainLaunch L) {
+    const int chain = blockIdx.x;
+    const int64_t n = L.cnt[chain];
+    const double* y = L.descs[chain].y;
+    const double* z = L.zbuf64 + (int64_t)chain * L.zstride;
+    double acc = 0.0;
+    for (int64_t t = threadIdx.x; t < n; t += blockDim.x) {
+        double mult;
+        acc += gradient_scalar<G_LOGISTIC, double>(as_global(z)[t], as_global(y)[t], mult);
+    }
+    acc = wave_sum(acc);
+    __shared__ double part[16];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double s = 0.0;
+        for (int k = 0; k < 16; ++k) s += part[k];
+        L.loss[chain] = s;
+    }
+}
+
 // stepSize / math.sqrt(iter) for iter = 1..n (SGDUpdater.scala:93, :133, :174, :210, :261).
 __global__ void steps_kernel(double step, int64_t n, double* __restrict__ steps) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -639,6 +674,10 @@ static int launch_reg(const ChainLaunch& L, const KParams& kp, bool full, size_t
         auto k = chain_dense<S, T, GRAD, UPD, CONV, NV, false>;
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
         hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(128), bytes, st, L, kp, g);
+    }
+    if constexpr (GRAD == G_LOGISTIC && sizeof(T) == 8) {
+        if (!L.zbuf64) return (int)hipErrorInvalidValue;
+        hipLaunchKernelGGL(logistic_loss64_kernel, dim3(kp.n_chains), dim3(1024), 0, st, L);
     }
     return (int)hipGetLastError();
 }
