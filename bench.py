@@ -71,7 +71,10 @@ def pmc_traffic(workload, grad, variant, storage, rows):
 def kernel_name(variant):
     if 300 <= variant < 400:
         return f"chain_block (NV={variant - 300}: blocked fp32 chain, 8-row Gram blocks)"
-    if 400 <= variant < 500:
+    if 410 <= variant < 500:
+        return ("chain_sparse_spec (fp32 CSR chain, weights L2/MALL-resident, gathers 8 samples "
+                "ahead with an LDS feature-tag correction)")
+    if 400 <= variant < 410:
         return "chain_sparse (fp32 CSR chain, weights L2/MALL-resident, one gather round trip per sample)"
     if 100 <= variant < 200:
         return f"chain_dense (NV={variant - 100}: per-sample chain)"
