@@ -1,0 +1,30 @@
+"""bench.py's host-side helpers (no GPU): the roofline `traffic` field comes from the committed
+rocprofv3 PMC summaries in profiles/, matched to the launched kernel instance."""
+import bench
+
+
+def test_pmc_traffic_matches_committed_profiles():
+    t, src = bench.pmc_traffic("c2", "least_squares", 302, "f32", 10_000_000)
+    assert src and src.startswith("profiles/") and src.endswith("_c2_pmc.json")
+    # HBM bytes per launch within 1 % of the algorithmic (d + 1) * 4 B per row: no re-reads
+    assert abs(t / (10_000_000 * 513 * 4) - 1.0) < 0.01
+    t3, _ = bench.pmc_traffic("c3", "logistic", 304, "f32", 12_500_000)
+    assert abs(t3 / (12_500_000 * 1025 * 4) - 1.0) < 0.01
+
+
+def test_pmc_traffic_none_for_unprofiled_kernels():
+    assert bench.pmc_traffic("c1", "logistic", 101, "f64", 100_000) == (None, None)
+
+
+def test_kernel_labels():
+    assert bench.kernel_name(302).startswith("chain_block (NV=2")
+    assert bench.kernel_name(411).startswith("chain_sparse_spec")
+    assert bench.kernel_name(401).startswith("chain_sparse (")
+    assert bench.kernel_name(101).startswith("chain_dense")
+
+
+def test_workloads_cover_the_baseline_configs():
+    assert set(bench.WORKLOADS) == {"c1", "c2", "c3", "c4", "c5"}
+    grad, n, d, P, step, sdt, _ = bench.WORKLOADS["c2"]
+    assert (grad, n, d, P, sdt) == ("least_squares", 10_000_000, 512, 256, "f32")
+    assert bench.WORKLOADS["c1"][:4] == ("logistic", 100_000, 100, 4)
