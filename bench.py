@@ -203,6 +203,19 @@ def cpu_baseline(grad, d, P, step, budget_s, seed=7, csr_nnz=0):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` on its own: start the N ranks as children (torchrun's
+        # launcher, 127.0.0.1 rendezvous) and exit with their status; nothing here has touched
+        # the GPU yet
+        import socket
+        import subprocess
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+               "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.run(cmd).returncode)
     import torch
     import torch.distributed as dist
     import __graft_entry__ as ge
