@@ -48,11 +48,13 @@ def pmc_traffic(workload, grad, variant, storage, rows):
     tools/pmc_summary.py; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM), or None."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_pmc.json")))
-    if not files or not (300 <= variant < 500):
+    if not files or not (300 <= variant < 600):
         return None, None
     g = {"logistic": 0, "least_squares": 1, "hinge": 2}[grad]
     sname = "float" if storage == "f32" else "double"
-    if variant >= 410:
+    if variant >= 500:
+        prefix = f"psgd::chain_block64<{sname}, {g}, 0, {variant - 500},"
+    elif variant >= 410:
         prefix = f"psgd::chain_sparse_spec<{sname}, {g}, 0>"
     elif variant >= 400:
         prefix = f"psgd::chain_sparse<{sname}, {g}, 0>"
@@ -71,6 +73,8 @@ def pmc_traffic(workload, grad, variant, storage, rows):
 def kernel_name(variant):
     if 300 <= variant < 400:
         return f"chain_block (NV={variant - 300}: blocked fp32 chain, 8-row Gram blocks)"
+    if 500 <= variant < 600:
+        return f"chain_block64 (NV={variant - 500}: blocked fp64 chain, 8-row Gram blocks)"
     if 410 <= variant < 500:
         return ("chain_sparse_spec (fp32 CSR chain, weights L2/MALL-resident, gathers 8 samples "
                 "ahead with an LDS feature-tag correction)")
@@ -203,18 +207,20 @@ def cpu_baseline(grad, d, P, step, budget_s, seed=7, csr_nnz=0):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']} "
+                 "(the launcher and the flag disagree)")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # `python bench.py --gpus N` on its own: start the N ranks as children (torchrun's
-        # launcher, 127.0.0.1 rendezvous) and exit with their status; nothing here has touched
-        # the GPU yet
-        import socket
+        # launcher; it picks the rendezvous port itself on 127.0.0.1) and exit with their
+        # status. Under a profiler its preloaded library has already initialised the GPU in
+        # this process: launching from here would be a launcher hop under the profiler, so
+        # profile one rank instead.
+        if "rocprof" in os.environ.get("LD_PRELOAD", "") or any(k.startswith("ROCPROF") for k in os.environ):
+            sys.exit("bench.py: --gpus > 1 under rocprofv3 is refused; profile a single rank (--gpus 1)")
         import subprocess
-        with socket.socket() as sk:
-            sk.bind(("127.0.0.1", 0))
-            port = sk.getsockname()[1]
-        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-               f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
-               "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
+               f"--nproc-per-node={args.gpus}", os.path.abspath(__file__)] + sys.argv[1:]
         sys.exit(subprocess.run(cmd).returncode)
     import torch
     import torch.distributed as dist

@@ -1,0 +1,581 @@
+// psgd_block64.hip -- the blocked chain kernel of the fp64 parity mode (gfx950).
+//
+// Reference: ParallelizedSGD.scala:243-270 (the chain), [ext] MLlib 1.6.1 Gradient.scala
+// (Logistic / LeastSquares / Hinge, called at ParallelizedSGD.scala:254), SGDUpdater.scala:86-98
+// (SimpleSGDUpdater) and :163-181 (SquaredL2SGDUpdater); all in Double, as here.
+//
+// Same recurrence as the fp32 chain_block (psgd_block.hip): over a block of K = 8 consecutive
+// rows with weights W at its start,
+//
+//     z_k = x_k . W + sum_{i<k} c_i (x_k . x_i)          (SquaredL2: z <- a_i z + c_i G[k][i])
+//     W'  = a_{K-1}(...(a_0 W + c_0 x_0)...) + c_{K-1} x_{K-1}
+//
+// with c_i = -s_i * mult(z_i, y_i), s_i = stepSize/sqrt(j), a_i = 1 - s_i*lambda. Every quantity is
+// a double: the K dots against W, the Gram triangle (products of the stored values are exact in
+// f64 for f32 rows), the scalar recurrence with the reference's multipliers (exp and the division
+// of LogisticGradient in f64), the updates. Only sums are reassociated (the wave tree of each dot,
+// the Gram identity above, the fused c*x + w update), which is the fp64 mode's 1e-9 relative bar
+// (DESIGN.md §4); per-chain counts are exact because this kernel runs only without the per-sample
+// convergence test (tol = 0). With tol > 0, and for L1/AdaGrad/Adam, the per-sample kernels of
+// psgd_kernels.hip run.
+//
+// Why blocks in fp64: the per-sample kernel (chain_dense) has the dot's wave reduction, an f64
+// exp and a division and the update on one dependent path per sample (~400 ns at d = 100). Here
+// only the scalar recurrence is sequential per sample; the dots, the Gram triangle and the
+// updates are batched over 8 rows and spread over three waves on three SIMDs.
+//
+// One workgroup = one chain = four waves, one per SIMD:
+//   wave 0 (chain)   owns W (doubles in VGPRs: lane l holds features (v*64+l)*VEC ..), per block:
+//                    the 8 dots, one transposed 8-value reduction, the recurrence, the loss terms,
+//                    the 8 updates;
+//   wave 1 (loader)  the LDS-DMA row ring of chain_dense/chain_block (ring_loader);
+//   waves 2, 3 (Gram) alternate blocks: the 28 pair dots of a block in f64 (rows converted from
+//                    the storage type), one transposed 32-value reduction, an 8x8 lower-triangular
+//                    f64 slot in LDS.
+// No MFMA: the triangle is 3.5 dots per row (an f64 16x16x4 MFMA tile would spend 16).
+#include "psgd_device.h"
+
+namespace psgd {
+
+namespace {
+
+constexpr int kB = 8;            // rows per block
+constexpr int kPairs = 28;       // kB*(kB-1)/2
+static_assert(kMetaRows == 2 * kB, "a meta block holds two row blocks");
+
+struct GramHeader64 {
+    unsigned gdone[2];   // blocks finished by Gram wave 0 (even blocks) / 1 (odd blocks)
+    unsigned gread[2];   // blocks whose rows Gram wave 0 / 1 has read (their ring slots are free)
+};
+
+__device__ __forceinline__ unsigned lo32(double v) { return (unsigned)(unsigned long long)__double_as_longlong(v); }
+__device__ __forceinline__ unsigned hi32(double v) { return (unsigned)((unsigned long long)__double_as_longlong(v) >> 32); }
+__device__ __forceinline__ double mk64(unsigned lo, unsigned hi) {
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// Transposed wave reductions on doubles (both 32-bit halves permuted alike), as reduce8 /
+// reduce32 of psgd_block.hip: each stage halves the values a lane carries.
+__device__ __forceinline__ double pair32d(double x, double y) {
+    auto pl = __builtin_amdgcn_permlane32_swap(lo32(x), lo32(y), false, false);
+    auto ph = __builtin_amdgcn_permlane32_swap(hi32(x), hi32(y), false, false);
+    return mk64(pl[0], ph[0]) + mk64(pl[1], ph[1]);
+}
+__device__ __forceinline__ double pair16d(double x, double y) {
+    auto pl = __builtin_amdgcn_permlane16_swap(lo32(x), lo32(y), false, false);
+    auto ph = __builtin_amdgcn_permlane16_swap(hi32(x), hi32(y), false, false);
+    return mk64(pl[0], ph[0]) + mk64(pl[1], ph[1]);
+}
+template <int CTRL, int BIT>
+__device__ __forceinline__ double pair_dppd(double x, double y, int lane) {
+    const bool hi = (lane & BIT) != 0;
+    const double keep = hi ? y : x;
+    const double send = hi ? x : y;
+    return keep + dpp_mov<CTRL>(send);
+}
+
+// 8 values -> lane l holds the total of value k(l) = l5 | l4<<1 | l3<<2.
+__device__ __forceinline__ double reduce8d(const double (&v)[8], int lane) {
+    const double a0 = pair32d(v[0], v[1]), a1 = pair32d(v[2], v[3]);
+    const double a2 = pair32d(v[4], v[5]), a3 = pair32d(v[6], v[7]);
+    const double b0 = pair16d(a0, a1), b1 = pair16d(a2, a3);
+    double r = pair_dppd<0x140, 8>(b0, b1, lane);   // row_mirror: partner l^15
+    r = r + dpp_mov<0xB1>(r);                        // quad_perm [1,0,3,2]: l^1
+    r = r + dpp_mov<0x4E>(r);                        // quad_perm [2,3,0,1]: l^2
+    r = r + dpp_mov<0x141>(r);                       // row_half_mirror: l^7
+    return r;
+}
+// 32 values -> lane l holds the total of value j(l) = l5 | l4<<1 | l3<<2 | l2<<3 | l1<<4.
+__device__ __forceinline__ double reduce32d(const double (&v)[32], int lane) {
+    double a[16], b[8], c[4], e[2];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) a[m] = pair32d(v[2 * m], v[2 * m + 1]);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) b[m] = pair16d(a[2 * m], a[2 * m + 1]);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) c[m] = pair_dppd<0x140, 8>(b[2 * m], b[2 * m + 1], lane);   // l^15
+#pragma unroll
+    for (int m = 0; m < 2; ++m) e[m] = pair_dppd<0x141, 4>(c[2 * m], c[2 * m + 1], lane);   // l^7
+    double r = pair_dppd<0x4E, 2>(e[0], e[1], lane);                                          // l^2
+    return r + dpp_mov<0xB1>(r);                                                              // l^1
+}
+
+// Lane that carries row i of a block after reduce8d (one with k(l) = i and l&7 = 0).
+__host__ __device__ constexpr int row_lane64(int i) {
+    return 32 * (i & 1) + 16 * ((i >> 1) & 1) + 8 * ((i >> 2) & 1);
+}
+
+// c = (-s) * mult(z, y): the step the row's gradient takes ([ext] MLlib 1.6.1 Gradient.compute,
+// SGDUpdater.scala:95 / :178 axpy(-thisIterStepSize, gradient, w)).
+//   Logistic: mult = 1/(1 + exp(-z)) - y;  LeastSquares: mult = z - y;
+//   Hinge: mult = 1 > ls*z ? -ls : 0 (ls = 2y - 1; the empty gradient adds nothing)
+template <int GRAD>
+__device__ __forceinline__ double coef64(double z, double y, double ns) {
+    if constexpr (GRAD == G_LEAST_SQUARES) {
+        return ns * (z - y);
+    } else if constexpr (GRAD == G_LOGISTIC) {
+        const double margin = -z;
+        return ns * ((1.0 / (1.0 + exp(margin))) - y);
+    } else {
+        const double ls = 2.0 * y - 1.0;
+        return (1.0 > ls * z) ? ns * (-ls) : 0.0;
+    }
+}
+
+// The row's loss ([ext] MLlib 1.6.1): LeastSquares diff*diff/2.0; Hinge 1 - ls*z or 0.
+// (Logistic's loss is evaluated after the chain from the stored z, logistic_loss64_kernel.)
+template <int GRAD>
+__device__ __forceinline__ double row_loss64(double z, double y) {
+    if constexpr (GRAD == G_LEAST_SQUARES) {
+        const double diff = z - y;
+        return diff * diff / 2.0;
+    } else {
+        const double ls = 2.0 * y - 1.0;
+        const double lz = ls * z;
+        return (1.0 > lz) ? 1.0 - lz : 0.0;
+    }
+}
+
+}  // namespace
+
+template <typename S, int GRAD, int UPD, int NV, bool FULL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
+    using V = typename Vec16<S>::type;
+    constexpr int VEC = Vec16<S>::N;
+    constexpr int E = NV * VEC;            // features per lane
+    constexpr int ROW_BYTES = NV * 1024;
+    constexpr bool KEEP = E <= 8;          // the chain wave keeps a block's rows in registers
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    // LDS: [RingHeader 16 B][GramHeader64 16 B][meta ring MB x 256 B][Gram ring GS x 512 B]
+    //      [row ring R x ROW_BYTES]
+    RingHeader* hdr = reinterpret_cast<RingHeader*>(smem);
+    GramHeader64* ghdr = reinterpret_cast<GramHeader64*>(smem + sizeof(RingHeader));
+    char* meta_ring = smem + sizeof(RingHeader) + sizeof(GramHeader64);
+    double* gring = reinterpret_cast<double*>(meta_ring + geom.meta_blocks * kMetaBlockBytes);
+    const int GS = geom.gslots;
+    char* ring = reinterpret_cast<char*>(gring + GS * kB * kB);
+
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int chain = blockIdx.x;
+    const ChainDesc dsc = L.descs[chain];
+    const int d = kp.d;
+    const int64_t n = dsc.n_rows;
+    const int R = geom.rows;               // multiple of kB: a block never wraps
+    const int MB = geom.meta_blocks;
+    const int64_t nblk = (n + kB - 1) / kB;
+
+    if (threadIdx.x == 0) {
+        hdr->ready = 0;
+        hdr->consumed = 0;
+        hdr->stop = 0;
+        ghdr->gdone[0] = 0;
+        ghdr->gdone[1] = 0;
+        ghdr->gread[0] = 0;
+        ghdr->gread[1] = 0;
+    }
+    // entries on and above the diagonal stay zero (the Gram waves write only i < k)
+    for (int i = threadIdx.x; i < GS * kB * kB; i += blockDim.x) gring[i] = 0.0;
+    __syncthreads();
+
+    if (wave == 1) {
+        ring_loader<S, NV, FULL, kB, kB>(L, dsc, hdr, meta_ring, ring, geom, lane, ghdr->gread);
+        return;
+    }
+
+    // Wait until `rows` rows have landed. false (and the watchdog) if nothing moves for 4 s.
+    auto wait_ready = [&](unsigned& ready, int64_t rows, int code) __attribute__((always_inline)) -> bool {
+        if (rows <= (int64_t)ready) return true;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            ready = __hip_atomic_load(&hdr->ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (rows <= (int64_t)ready) return true;
+            if (__hip_atomic_load(&hdr->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kWatchdogTicks) {
+                __hip_atomic_fetch_or(L.watchdog, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                return false;
+            }
+            if (code != 2) __builtin_amdgcn_s_sleep(1);   // the chain wave polls without sleeping
+        }
+    };
+    // One 16-byte vector of a row slot as doubles, zero past the row end (stale LDS bytes).
+    auto read_vec = [&](const char* slot, int v, double* out) __attribute__((always_inline)) {
+        V xv = *reinterpret_cast<const V*>(slot + v * 1024 + lane * 16);
+        if constexpr (!FULL) {
+            if ((v * 64 + lane) * VEC >= dsc.ld) xv = V(0);
+        }
+        unpack<S, double>(xv, out);
+    };
+
+    if (wave >= 2) {
+        // ---------------- Gram waves ----------------
+        const int gw = wave - 2;
+        const int j = ((lane >> 5) & 1) | (((lane >> 4) & 1) << 1) | (((lane >> 3) & 1) << 2) |
+                      (((lane >> 2) & 1) << 3) | (((lane >> 1) & 1) << 4);
+        int goff = -1;   // this lane's (k, i) after reduce32d, as an offset into an 8x8 slot
+        {
+            int jj = 0;
+            for (int k = 1; k < kB; ++k)
+                for (int i = 0; i < k; ++i, ++jj)
+                    if (jj == j) goff = k * kB + i;
+            if (lane & 1) goff = -1;
+        }
+        unsigned ready = 0;
+        unsigned done = 0;
+        int rs = gw * kB;            // ring slot of the block's first row (R is a multiple of 16)
+        int gs = gw;                 // Gram slot of the block
+        for (int64_t b = gw; b < nblk; b += 2) {
+            const int64_t t0 = b * kB;
+            const int64_t kk = (n - t0) < kB ? (n - t0) : kB;
+            if (!wait_ready(ready, t0 + kk, 4)) break;
+            const char* base = ring + rs * ROW_BYTES;
+            rs += 2 * kB;
+            if (rs >= R) rs -= R;
+            double acc[kPairs];
+#pragma unroll
+            for (int q = 0; q < kPairs; ++q) acc[q] = 0.0;
+            // one 16-byte vector of every row at a time (f64 rows of a whole block would not
+            // fit the registers at NV >= 4)
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                double xc[kB][VEC];
+#pragma unroll
+                for (int k = 0; k < kB; ++k) read_vec(base + k * ROW_BYTES, v, xc[k]);
+                int q = 0;
+#pragma unroll
+                for (int k = 1; k < kB; ++k)
+#pragma unroll
+                    for (int i = 0; i < k; ++i, ++q)
+#pragma unroll
+                        for (int h = 0; h < VEC; ++h) acc[q] = __builtin_fma(xc[k][h], xc[i][h], acc[q]);
+            }
+            // every row of the block has been read: hand its ring slots back
+            asm volatile("s_waitcnt lgkmcnt(0)" : : : "memory");
+            __hip_atomic_store(&ghdr->gread[gw], done + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            double g[32];
+#pragma unroll
+            for (int q = 0; q < kPairs; ++q) g[q] = acc[q];
+#pragma unroll
+            for (int q = kPairs; q < 32; ++q) g[q] = 0.0;
+            const double val = reduce32d(g, lane);
+            double* slot = gring + gs * (kB * kB);
+            gs += 2;
+            if (gs >= GS) gs -= GS;
+            if (goff >= 0) slot[goff] = val;
+            ++done;
+            __hip_atomic_store(&ghdr->gdone[gw], done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        return;
+    }
+
+    // ---------------- chain wave ----------------
+    double w[E];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const int base = (v * 64 + lane) * VEC;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            const int f = base + k;
+            const double wv = as_global(L.w_in)[f < d ? f : 0];
+            w[v * VEC + k] = f < d ? wv : 0.0;
+        }
+    }
+    const int krow = ((lane >> 5) & 1) | (((lane >> 4) & 1) << 1) | (((lane >> 3) & 1) << 2);
+    const bool loss_lane = (lane & 7) == 0;   // one copy of every row's loss
+    // Logistic: the rows' dots go to L.zbuf64 and logistic_loss64_kernel sums their losses after
+    // the chain (log1pExp is a second exp and a log1p; off the sequential wave)
+    constexpr bool LOSS_EXT = GRAD == G_LOGISTIC;
+    gmut<double> zout = as_global_mut(L.zbuf64 + (LOSS_EXT ? (int64_t)chain * L.zstride : 0));
+    const double lam = kp.reg;
+    double loss_sum = 0.0;
+    int64_t count = 0;
+    unsigned ready = 0;
+    int rs = 0, gs = 0, ms = 0;      // ring slot, Gram slot and meta block of the current block
+    const int64_t nfull = n / kB;
+    const int ntail = (int)(n - nfull * kB);
+
+    auto wait_rows = [&](int64_t rows) __attribute__((always_inline)) -> bool {
+        return wait_ready(ready, rows, 2);
+    };
+    // A block's rows from the ring into registers; rows >= kk (a tail block) read as zero.
+    auto load_rows = [&](auto tail_c, double (&xr)[kB][E], const char* base, int kk) __attribute__((always_inline)) {
+        constexpr bool TAIL = decltype(tail_c)::value;
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                double xv[VEC];
+                read_vec(base + k * ROW_BYTES, v, xv);
+#pragma unroll
+                for (int h = 0; h < VEC; ++h) xr[k][v * VEC + h] = (TAIL && k >= kk) ? 0.0 : xv[h];
+            }
+        }
+    };
+
+    // One block: rows in xr (KEEP) or in the ring at `base`; kk rows (kB unless TAIL).
+    auto block = [&](auto tail_c, double (&xr)[kB][E], int64_t b, int kk, const char* base)
+                     __attribute__((always_inline)) -> bool {
+        constexpr bool TAIL = decltype(tail_c)::value;
+        const int64_t t0 = b * kB;
+        // this lane's row: label and stepSize/sqrt(j)
+        const f64x2 meta = *reinterpret_cast<const f64x2*>(
+            meta_ring + ms * kMetaBlockBytes + ((int)(b & 1) * kB + krow) * 16);
+        if constexpr (KEEP) {
+            // rows are in registers (the Gram and meta slots are reused only after the next
+            // block is handed back): free the ring slots (the loader also waits for the Gram)
+            __hip_atomic_store(&hdr->consumed, (unsigned)(t0 + kk), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        // flags this block tests, read now so that their LDS round trip lands under the dots
+        const unsigned gpre = __hip_atomic_load(&ghdr->gdone[b & 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const unsigned rpre = __hip_atomic_load(&hdr->ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // p_k = x_k . W
+        double pk[kB];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+            double a = 0.0;
+            if constexpr (KEEP) {
+#pragma unroll
+                for (int e = 0; e < E; ++e) a = __builtin_fma(xr[k][e], w[e], a);
+            } else {
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    double xv[VEC];
+                    read_vec(base + k * ROW_BYTES, v, xv);
+#pragma unroll
+                    for (int h = 0; h < VEC; ++h) a = __builtin_fma(xv[h], w[v * VEC + h], a);
+                }
+            }
+            pk[k] = a;
+        }
+        const double yv = meta.x, sv = meta.y;
+        const double nsv = -sv;
+        const double alpha = 1.0 - sv * lam;      // SquaredL2 shrink of this lane's row (UPD:169)
+        double z = reduce8d(pk, lane);
+        // the block's Gram triangle (Gram wave b&1 publishes its blocks in order)
+        {
+            const unsigned need = (unsigned)(b >> 1) + 1;
+            unsigned* gd = &ghdr->gdone[b & 1];
+            if (gpre < need) {
+                const uint64_t tw = __builtin_amdgcn_s_memrealtime();
+                while (__hip_atomic_load(gd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+                    if (__builtin_amdgcn_s_memrealtime() - tw > kWatchdogTicks) {
+                        __hip_atomic_fetch_or(L.watchdog, 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        return false;
+                    }
+                }
+            }
+        }
+        const double* grow = gring + gs * (kB * kB) + krow * kB;
+        double G[kB];
+#pragma unroll
+        for (int q = 0; q < kB / 2; ++q) {
+            const f64x2 g2 = *reinterpret_cast<const f64x2*>(grow + 2 * q);
+            G[2 * q] = g2.x;
+            G[2 * q + 1] = g2.y;
+        }
+
+        // the scalar recurrence: c_i from z_i, then every later row's dot moves by c_i G[k][i]
+        // (SquaredL2 also shrinks the finished rows' z: zf keeps z_k for the loss)
+        double c[kB], al[kB];
+        double zf = z;
+#pragma unroll
+        for (int i = 0; i < kB; ++i) {
+            c[i] = readlane_d(coef64<GRAD>(z, yv, nsv), row_lane64(i));
+            if constexpr (TAIL) c[i] = i < kk ? c[i] : 0.0;
+            if constexpr (UPD == U_SQUARED_L2) {
+                if (krow == i) zf = z;
+                al[i] = readlane_d(alpha, row_lane64(i));
+                if constexpr (TAIL) al[i] = i < kk ? al[i] : 1.0;
+                if (i + 1 < kB) z = __builtin_fma(c[i], G[i], al[i] * z);
+            } else {
+                if (i + 1 < kB) z = __builtin_fma(c[i], G[i], z);
+            }
+        }
+        if constexpr (UPD != U_SQUARED_L2) zf = z;
+        if constexpr (LOSS_EXT) {
+            if (loss_lane && (!TAIL || krow < kk)) zout[t0 + krow] = zf;
+        } else {
+            const double l = row_loss64<GRAD>(zf, yv);
+            if (loss_lane && (!TAIL || krow < kk)) loss_sum += l;
+        }
+        count += kk;
+        if (rpre > ready) ready = rpre;
+
+        // W <- a_i W + c_i x_i, i = 0..kk-1, in sample order
+#pragma unroll
+        for (int i = 0; i < kB; ++i) {
+            if constexpr (KEEP) {
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    if constexpr (UPD == U_SQUARED_L2) w[e] = __builtin_fma(c[i], xr[i][e], w[e] * al[i]);
+                    else w[e] = __builtin_fma(c[i], xr[i][e], w[e]);
+                }
+            } else if (!TAIL || i < kk) {
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    double xv[VEC];
+                    read_vec(base + i * ROW_BYTES, v, xv);
+#pragma unroll
+                    for (int h = 0; h < VEC; ++h) {
+                        const int e = v * VEC + h;
+                        if constexpr (UPD == U_SQUARED_L2) w[e] = __builtin_fma(c[i], xv[h], w[e] * al[i]);
+                        else w[e] = __builtin_fma(c[i], xv[h], w[e]);
+                    }
+                }
+            }
+        }
+        if constexpr (!KEEP) {
+            __hip_atomic_store(&hdr->consumed, (unsigned)(t0 + kk), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        rs += kB;
+        if (rs == R) rs = 0;
+        if (++gs == GS) gs = 0;
+        if ((b & 1) && ++ms == MB) ms = 0;
+        return true;
+    };
+
+    using Full = std::integral_constant<bool, false>;
+    using Tail = std::integral_constant<bool, true>;
+    double xr[kB][E];
+    bool ok = true;
+    for (int64_t b = 0; ok && b < nfull; ++b) {
+        ok = wait_rows((b + 1) * kB);
+        if (!ok) break;
+        const char* base = ring + rs * ROW_BYTES;
+        if constexpr (KEEP) load_rows(Full{}, xr, base, kB);
+        ok = block(Full{}, xr, b, kB, base);
+    }
+    if (ok && ntail > 0 && wait_rows(n)) {
+        const char* base = ring + rs * ROW_BYTES;
+        if constexpr (KEEP) load_rows(Tail{}, xr, base, ntail);
+        block(Tail{}, xr, nfull, ntail, base);
+    }
+    // a wave that stopped early leaves the others blocked on it: wake them
+    __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    loss_sum = wave_sum(loss_sum);   // the 8 loss lanes' partials
+
+    // regVal of the chain's last update (PSGD.scala:257; 0.0 if no sample, :247)
+    double rv = 0.0;
+    if constexpr (UPD == U_SQUARED_L2) {
+        double acc = 0.0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc += w[e] * w[e];
+        acc = wave_sum(acc);
+        if (count > 0) {
+            const double nrm = sqrt(acc);
+            rv = 0.5 * kp.reg * nrm * nrm;
+        }
+    }
+
+    double* wo = L.w_out + (int64_t)chain * d;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const int base = (v * 64 + lane) * VEC;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k)
+            if (base + k < d) wo[base + k] = w[v * VEC + k];
+    }
+    if (lane == 0) {
+        L.rv[chain] = rv;
+        if constexpr (!LOSS_EXT) L.loss[chain] = loss_sum;
+        L.cnt[chain] = count;
+        L.cnt_d[chain] = double(count);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Launcher.
+// ------------------------------------------------------------------------------------------
+template <typename S, int GRAD, int UPD, int NV>
+static int launch_block64(const ChainLaunch& L, const KParams& kp, bool full, size_t lds, hipStream_t st) {
+    constexpr int ROW = NV * 1024;
+    const size_t budget = lds > 0 ? lds : (size_t)64 * 1024;
+    const size_t fixed = sizeof(RingHeader) + sizeof(GramHeader64);
+    const int D = loader_depth<NV>();
+    auto bytes_for = [&](int r) {
+        const int mb = (r + kMetaRows - 1) / kMetaRows + 2;
+        const int gs = r / kB + 1;
+        return fixed + (size_t)mb * kMetaBlockBytes + (size_t)gs * kB * kB * 8 + (size_t)r * ROW;
+    };
+    int R = (int)((budget - fixed) / ROW) / kB * kB;
+    while (R > 0 && bytes_for(R) > budget) R -= kB;
+    if (R < 2 * kB) return (int)hipErrorInvalidValue;   // LDS budget too small for this d
+    const int MB = (R + kMetaRows - 1) / kMetaRows + 2;
+    const int GS = R / kB + 1;
+    RingGeom g{R, MB, D, GS};
+    const size_t bytes = bytes_for(R);
+    if (full) {
+        auto k = chain_block64<S, GRAD, UPD, NV, true>;
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(256), bytes, st, L, kp, g);
+    } else {
+        auto k = chain_block64<S, GRAD, UPD, NV, false>;
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(256), bytes, st, L, kp, g);
+    }
+    if constexpr (GRAD == G_LOGISTIC) {
+        const int e = launch_logistic_loss64(L, kp.n_chains, st);
+        if (e) return e;
+    }
+    return (int)hipGetLastError();
+}
+
+template <typename S, int GRAD, int UPD>
+static int block64_nv(const ChainLaunch& L, const KParams& kp, int64_t min_ld, int64_t max_ld,
+                      size_t lds, hipStream_t st, int* variant) {
+    constexpr int VEC = 16 / sizeof(S);
+    int nv = 1;
+    while (nv * 64 * VEC < max_ld) nv *= 2;
+    const bool full = min_ld >= (int64_t)nv * 64 * VEC;
+    if (variant) *variant = 500 + nv;
+    switch (nv) {
+    case 1: return launch_block64<S, GRAD, UPD, 1>(L, kp, full, lds, st);
+    case 2: return launch_block64<S, GRAD, UPD, 2>(L, kp, full, lds, st);
+    case 4: return launch_block64<S, GRAD, UPD, 4>(L, kp, full, lds, st);
+    case 8: return launch_block64<S, GRAD, UPD, 8>(L, kp, full, lds, st);
+    default: return -3;
+    }
+}
+
+template <typename S, int GRAD>
+static int block64_upd(const ChainLaunch& L, const KParams& kp, int upd, int64_t min_ld,
+                       int64_t max_ld, size_t lds, hipStream_t st, int* variant) {
+    if (upd == U_SIMPLE) return block64_nv<S, GRAD, U_SIMPLE>(L, kp, min_ld, max_ld, lds, st, variant);
+    if (upd == U_SQUARED_L2) return block64_nv<S, GRAD, U_SQUARED_L2>(L, kp, min_ld, max_ld, lds, st, variant);
+    return -3;
+}
+
+template <typename S>
+static int block64_grad(const ChainLaunch& L, const KParams& kp, int grad, int upd, int64_t min_ld,
+                        int64_t max_ld, size_t lds, hipStream_t st, int* variant) {
+    switch (grad) {
+    case G_LOGISTIC: return block64_upd<S, G_LOGISTIC>(L, kp, upd, min_ld, max_ld, lds, st, variant);
+    case G_LEAST_SQUARES: return block64_upd<S, G_LEAST_SQUARES>(L, kp, upd, min_ld, max_ld, lds, st, variant);
+    case G_HINGE: return block64_upd<S, G_HINGE>(L, kp, upd, min_ld, max_ld, lds, st, variant);
+    default: return -3;
+    }
+}
+
+bool block64_path_applies(int layout, int compute, int updater, bool check_conv, int storage,
+                          int64_t max_ld) {
+    const int vec = storage == 1 ? 4 : 2;
+    return layout == kDense && compute == 0 && !check_conv &&
+           (updater == U_SIMPLE || updater == U_SQUARED_L2) && max_ld <= 8 * 64 * vec;
+}
+
+int launch_block64_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
+                          int updater, int64_t min_ld, int64_t max_ld, int lds_spread,
+                          hipStream_t stream, int* kernel_variant) {
+    if (kp.n_chains <= 0) return 0;
+    if (gradient == G_LOGISTIC && !L.zbuf64) return (int)hipErrorInvalidValue;
+    const size_t lds = (size_t)(lds_spread > 0 ? lds_spread : 0);
+    if (storage == 1)
+        return block64_grad<float>(L, kp, gradient, updater, min_ld, max_ld, lds, stream, kernel_variant);
+    return block64_grad<double>(L, kp, gradient, updater, min_ld, max_ld, lds, stream, kernel_variant);
+}
+
+}  // namespace psgd

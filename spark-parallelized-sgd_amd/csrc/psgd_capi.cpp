@@ -520,7 +520,9 @@ int32_t psgd_clear_partitions(psgd_ctx* ctx) {
     if (!ctx) return fail(PSGD_EINVAL, "ctx is null");
     std::lock_guard<std::mutex> lk(ctx->mu);
     DeviceGuard g(ctx->device);
-    hipStreamSynchronize(ctx->stream);
+    // epochs may run on caller streams (psgd_run_epoch_device): drain the device, not just the
+    // context's stream, before the partitions' buffers go
+    hipDeviceSynchronize();
     for (auto& kv : ctx->parts) free_part(kv.second);
     ctx->parts.clear();
     ctx->descs_dirty = true;

@@ -74,6 +74,15 @@ bool block_path_applies(int layout, int compute, int updater, bool check_conv, i
 int launch_block_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
                         int updater, int64_t min_ld, int64_t max_ld, int lds_spread,
                         hipStream_t stream, int* kernel_variant);
+// The blocked fp64 kernel (psgd_block64.hip): dense rows, Simple/SquaredL2, fp64 compute, no
+// per-sample convergence test (the parity mode's throughput kernel). -3 when it does not apply.
+bool block64_path_applies(int layout, int compute, int updater, bool check_conv, int storage,
+                          int64_t max_ld);
+int launch_block64_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
+                          int updater, int64_t min_ld, int64_t max_ld, int lds_spread,
+                          hipStream_t stream, int* kernel_variant);
+// lossSum of fp64 Logistic chains from the per-row dots in L.zbuf64 (psgd_kernels.hip).
+int launch_logistic_loss64(const ChainLaunch& L, int n_chains, hipStream_t stream);
 int launch_fold(const double* w, int64_t w_stride, const double* rv, const double* loss,
                 const double* cnt, int64_t s_stride, int n, int d, double* out,
                 const int* watchdog, hipStream_t stream);

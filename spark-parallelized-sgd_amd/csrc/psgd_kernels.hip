@@ -682,6 +682,12 @@ static int launch_reg(const ChainLaunch& L, const KParams& kp, bool full, size_t
     return (int)hipGetLastError();
 }
 
+int launch_logistic_loss64(const ChainLaunch& L, int n_chains, hipStream_t st) {
+    if (!L.zbuf64) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(logistic_loss64_kernel, dim3(n_chains), dim3(1024), 0, st, L);
+    return (int)hipGetLastError();
+}
+
 template <typename S, typename T, int GRAD, int UPD, bool CONV>
 static int dispatch_nv(const ChainLaunch& L, const KParams& kp, int64_t min_ld, int64_t max_ld,
                        size_t lds, hipStream_t st, int* variant) {
@@ -760,11 +766,14 @@ int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int stora
     if (kp.n_chains <= 0) return 0;
     if (kp.nc > 0)   // LogisticGradient(numClasses > 2)
         return launch_multinomial_chains(L, kp, layout, storage, updater, check_conv, stream, kernel_variant);
-    // PSGD_PER_SAMPLE=1 keeps fp32 mode on the per-sample kernel (A/B measurements)
+    // PSGD_PER_SAMPLE=1 keeps the per-sample kernels (A/B measurements)
     static const bool per_sample = [] {
         const char* e = getenv("PSGD_PER_SAMPLE");
         return e && *e && *e != '0';
     }();
+    if (!per_sample && block64_path_applies(layout, compute, updater, check_conv, storage, max_ld))
+        return launch_block64_chains(L, kp, storage, gradient, updater, min_ld, max_ld, lds_spread,
+                                     stream, kernel_variant);
     if (!per_sample && block_path_applies(layout, compute, updater, check_conv, storage, max_ld))
         return launch_block_chains(L, kp, storage, gradient, updater, min_ld, max_ld, lds_spread,
                                    stream, kernel_variant);

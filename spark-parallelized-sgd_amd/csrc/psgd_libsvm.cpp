@@ -42,24 +42,67 @@ void trim(const char*& b, const char*& e) {
     while (e > b && (unsigned char)e[-1] <= ' ') --e;
 }
 
+// java.lang.Double.parseDouble (StringOps.toDouble) [ext JDK FloatingDecimal.readJavaFormatString]:
+// trimmed; optional sign; "NaN" or "Infinity" (exact case), or a decimal significand with at
+// least one digit ("1.", ".5") and an optional e/E exponent with at least one digit, or a hex
+// significand 0x/0X with a mandatory p/P binary exponent; then an optional f/F/d/D suffix and
+// nothing else. The value is the correctly rounded double (glibc strtod on the validated text;
+// the f/F suffix still yields the double -- parseDouble ignores the suffix's type).
 bool parse_double(const char* b, const char* e, double* out) {
-    std::string s(b, e);
-    if (s.empty()) return false;
-    char* end = nullptr;
-    errno = 0;
-    const double v = strtod(s.c_str(), &end);
-    if (end != s.c_str() + s.size()) return false;
-    *out = v;
+    trim(b, e);
+    const char* p = b;
+    bool neg = false;
+    if (p < e && (*p == '+' || *p == '-')) neg = *p++ == '-';
+    auto rest_is = [&](const char* word) {
+        const size_t k = strlen(word);
+        return (size_t)(e - p) == k && memcmp(p, word, k) == 0;
+    };
+    if (rest_is("NaN")) { *out = NAN; return true; }
+    if (rest_is("Infinity")) { *out = neg ? -INFINITY : INFINITY; return true; }
+    const char* q = p;
+    auto digits = [&](bool hex) {
+        const char* s0 = q;
+        while (q < e && (hex ? isxdigit((unsigned char)*q) : isdigit((unsigned char)*q))) ++q;
+        return (int)(q - s0);
+    };
+    const bool hex = (e - q) >= 2 && q[0] == '0' && (q[1] == 'x' || q[1] == 'X');
+    if (hex) q += 2;
+    int nd = digits(hex);
+    if (q < e && *q == '.') { ++q; nd += digits(hex); }
+    if (nd == 0) return false;
+    if (hex) {
+        if (!(q < e && (*q == 'p' || *q == 'P'))) return false;
+        ++q;
+        if (q < e && (*q == '+' || *q == '-')) ++q;
+        if (digits(false) == 0) return false;
+    } else if (q < e && (*q == 'e' || *q == 'E')) {
+        ++q;
+        if (q < e && (*q == '+' || *q == '-')) ++q;
+        if (digits(false) == 0) return false;
+    }
+    const char* num_end = q;
+    if (q < e && (*q == 'f' || *q == 'F' || *q == 'd' || *q == 'D')) ++q;
+    if (q != e) return false;
+    const std::string s(b, num_end);
+    *out = strtod(s.c_str(), nullptr);
     return true;
 }
 
+// java.lang.Integer.parseInt (StringOps.toInt): optional sign, one or more decimal digits,
+// nothing else (no whitespace), within int range.
 bool parse_int(const char* b, const char* e, int64_t* out) {
-    std::string s(b, e);
-    if (s.empty()) return false;
-    char* end = nullptr;
-    errno = 0;
-    const long long v = strtoll(s.c_str(), &end, 10);
-    if (end != s.c_str() + s.size() || errno == ERANGE || v > INT32_MAX || v < INT32_MIN) return false;
+    const char* p = b;
+    bool neg = false;
+    if (p < e && (*p == '+' || *p == '-')) neg = *p++ == '-';
+    if (p == e) return false;
+    int64_t v = 0;
+    for (; p < e; ++p) {
+        if (!isdigit((unsigned char)*p)) return false;
+        v = v * 10 + (*p - '0');
+        if (v > (int64_t)INT32_MAX + 1) return false;
+    }
+    v = neg ? -v : v;
+    if (v > INT32_MAX || v < INT32_MIN) return false;
     *out = v;
     return true;
 }

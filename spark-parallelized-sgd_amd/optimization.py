@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import logging
 import math
+import threading
 import uuid
 from typing import List, Optional, Tuple
 
@@ -87,6 +88,8 @@ def get_context(device: int) -> N.Context:
     if ctx is None:
         ctx = N.Context(device)
         ctx.registered_token = None
+        # serialises (re-)registration + epoch of the engines that share this device's context
+        ctx.engine_lock = threading.RLock()
         _contexts[device] = ctx
     return ctx
 
@@ -154,14 +157,20 @@ class HipEngine(ShardedEngine):
         self._gather = torch.empty(self.world * (self.d + 3), dtype=torch.float64, device=self.dev)
         self._folded = torch.empty(self.d + 3, dtype=torch.float64, device=self.dev)
         self._counts = torch.empty(max(self.n_local, 1), dtype=torch.int64, device=self.dev)
-        self._register(data)
+        self._data = data
+        with self.ctx.engine_lock:
+            self._register(data)
 
     def _register(self, data: PartitionedData):
+        """Register partitions [lo, hi) with the device context unless they are what it holds
+        (ctx.engine_lock held). Engines on one device share its context; the key records whose
+        partitions it holds."""
         token = getattr(data, "_psgd_token", None)
         if token is None:
             token = uuid.uuid4().hex
             data._psgd_token = token
         key = (token, self.lo, self.hi)
+        self._key = key
         if self.ctx.registered_token == key:
             return
         self.ctx.clear()
@@ -200,9 +209,13 @@ class HipEngine(ShardedEngine):
             return super().epoch(params, w_dev, with_counts)
 
     def local_partial(self, params, w_dev, with_counts):
-        self.ctx.run_epoch_device(params, w_dev.data_ptr(), self._partial.data_ptr(),
-                                  self._counts.data_ptr() if with_counts else None,
-                                  self.stream.cuda_stream)
+        with self.ctx.engine_lock:
+            # another engine on this device may have registered its own partitions since
+            if self.ctx.registered_token != self._key:
+                self._register(self._data)
+            self.ctx.run_epoch_device(params, w_dev.data_ptr(), self._partial.data_ptr(),
+                                      self._counts.data_ptr() if with_counts else None,
+                                      self.stream.cuda_stream)
         counts = self._counts[: self.n_local].cpu().numpy() if with_counts else None
         return self._partial, counts
 

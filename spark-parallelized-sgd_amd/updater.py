@@ -40,7 +40,7 @@ class L1SGDUpdater(SGDUpdater):
 
 class AdaGradSGDUpdater(SGDUpdater):
     """accum += g*g; w' = w - s * g / sqrt(accum + 1.0) (SGDUpdater.scala:193-228).
-    Per-chain status (accum) lives in HBM; dense rows only in this build."""
+    Per-chain status (accum) lives in HBM; dense and CSR rows."""
 
     kind = 3
 
@@ -48,7 +48,7 @@ class AdaGradSGDUpdater(SGDUpdater):
 class AdamSGDUpdater(SGDUpdater):
     """The reference's Adam variant, reproduced literally (SGDUpdater.scala:240-286):
     v = beta*v + (1-beta)*g; r = gamma*r + (1-gamma)*g*g;
-    w' = w - s/(1-beta^iter) * v / (sqrt(1 - r^iter) + eps).  Dense rows only in this build."""
+    w' = w - s/(1-beta^iter) * v / (sqrt(1 - r^iter) + eps).  Dense and CSR rows."""
 
     kind = 4
 

@@ -145,15 +145,19 @@ def test_dense_stateful_updaters(pkg, oracle, upd):
 
 
 def test_kernel_selection(pkg, oracle):
+    """fp64 compute: tol = 0 with Simple/SquaredL2 runs the blocked fp64 kernel (50x), tol > 0
+    the per-sample chain_dense (10x), d past the register-resident range chain_general (200)."""
     rng = np.random.default_rng(1)
-    for d, dtype, expect in ((100, np.float64, 101), (512, np.float32, 102), (1024, np.float32, 104),
-                             (3000, np.float64, 200)):
+    for d, dtype, tol, expect in ((100, np.float64, 0.0, 501), (512, np.float32, 0.0, 502),
+                                  (1024, np.float32, 0.0, 504), (2048, np.float32, 0.0, 508),
+                                  (100, np.float64, 0.001, 101), (512, np.float32, 0.001, 102),
+                                  (3000, np.float64, 0.0, 200)):
         X, y = synth(rng, 64, d, "logistic", dtype)
         data = pkg.PartitionedData.parallelize(y, X, 2, dtype=dtype)
         pkg.runParallelizedSGD(data, pkg.LogisticGradient(), pkg.SimpleSGDUpdater(), 1.0, 1, 0.0, 1.0,
-                               np.zeros(d), 0.0)
+                               np.zeros(d), tol)
         ctx = pkg.optimization.get_context(0)
-        assert ctx.last_kernel() == expect, (d, dtype, ctx.last_kernel())
+        assert ctx.last_kernel() == expect, (d, dtype, tol, ctx.last_kernel())
 
 
 def test_fp32_storage_fp64_compute(pkg, oracle):

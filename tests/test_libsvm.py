@@ -107,3 +107,52 @@ def test_libsvm_errors(pkg, tmp_path):
         pkg.loadLibSVMFile(str(f), 3)
     with pytest.raises(pkg.IllegalArgumentException):
         pkg.loadLibSVMFile(str(tmp_path / "missing.libsvm"))
+
+
+# java.lang.Double.parseDouble's grammar (StringOps.toDouble): accepted forms and their values,
+# and forms C's strtod takes that Java rejects
+JAVA_DOUBLES_OK = [("1.0d", 1.0), ("2f", 2.0), ("-3.5D", -3.5), ("+4F", 4.0), ("1.", 1.0), (".5", 0.5),
+                   ("1e3", 1000.0), ("1E-2", 0.01), ("NaN", float("nan")), ("-Infinity", float("-inf")),
+                   ("Infinity", float("inf")), ("0x1.8p1", 3.0), ("0X10P-4d", 1.0), ("-0", -0.0)]
+JAVA_DOUBLES_BAD = ["inf", "nan", "infinity", "INFINITY", "1e", "e5", ".", "0x1.8", "1.0dd", "1x", "--1",
+                    "0x", "1_0", "1.0e+"]
+
+
+@pytest.mark.parametrize("text,want", JAVA_DOUBLES_OK)
+def test_libsvm_java_double_forms(pkg, tmp_path, text, want):
+    f = tmp_path / "ok.libsvm"
+    f.write_bytes(f"{text} 2:{text}\n".encode())
+    data = pkg.loadLibSVMFile(str(f))
+    got_label, got_val = data.partitions[0].labels[0], data.partitions[0].val[0]
+    for got in (got_label, got_val):
+        if want != want:
+            assert got != got
+        else:
+            assert got == want and np.signbit(got) == np.signbit(want)
+
+
+@pytest.mark.parametrize("text", JAVA_DOUBLES_BAD)
+def test_libsvm_rejects_non_java_doubles(pkg, tmp_path, text):
+    f = tmp_path / "bad.libsvm"
+    f.write_bytes(f"1 3:{text}\n".encode())
+    with pytest.raises(pkg.IllegalArgumentException, match="NumberFormat"):
+        pkg.loadLibSVMFile(str(f))
+    f.write_bytes(f"{text} 3:1\n".encode())
+    with pytest.raises(pkg.IllegalArgumentException, match="NumberFormat"):
+        pkg.loadLibSVMFile(str(f))
+
+
+@pytest.mark.parametrize("text", ["+3", "0003"])
+def test_libsvm_java_int_forms(pkg, tmp_path, text):
+    f = tmp_path / "ok.libsvm"
+    f.write_bytes(f"1 {text}:2.5\n".encode())
+    data = pkg.loadLibSVMFile(str(f))
+    assert list(data.partitions[0].col) == [2]
+
+
+@pytest.mark.parametrize("text", ["3.0", "0x3", "2147483648", "1e1", "\t3"])
+def test_libsvm_rejects_non_java_ints(pkg, tmp_path, text):
+    f = tmp_path / "bad.libsvm"
+    f.write_bytes(f"1 {text}:2.5\n".encode())
+    with pytest.raises(pkg.IllegalArgumentException, match="NumberFormat"):
+        pkg.loadLibSVMFile(str(f))

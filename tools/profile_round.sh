@@ -10,6 +10,8 @@ export TMPDIR=/tmp
 OUT=gpurun_out/prof
 ARGS=${BENCH_ARGS:-"--no-cpu-baseline"}   # the bench defaults (5 timed steps, 2 warmup)
 mkdir -p $OUT
+# one rank only: bench.py --gpus N > 1 would start a launcher under the profiler
+case " $ARGS " in *" --gpus "[2-9]*|*" --gpus="[2-9]*) echo "profile a single rank (--gpus 1)"; exit 2;; esac
 step() { echo "== $1"; shift; "$@"; rc=$?; echo "rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
 step trace timeout -k 10 240 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- python3 bench.py $ARGS
 step fetch timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/fetch -o run -- python3 bench.py $ARGS
