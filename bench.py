@@ -39,20 +39,27 @@ WORKLOADS = {
 }
 CSR_NNZ = {"c4": 94, "c5": 100}  # nonzeros per row (c4: rcv1's mean; c5: SURVEY §8d)
 REG = {"c5": 1e-6}                # SquaredL2 regParam (c5); others: Simple updater
+# secondary lines: rows per GPU (0 = the workload's own; c5's full 125M-row shard takes minutes)
+SECONDARY_ROWS = {"c5": 20_000_000}
+DEFAULT_SECONDARY = "c3:f64,c3:f32,c2:f64,c1:f64,c4:f32"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def pmc_traffic(workload, grad, variant, storage, rows):
+def pmc_traffic(workload, grad, variant, storage, rows, compute="f32"):
     """HBM bytes per chain-kernel launch from the newest committed rocprofv3 PMC summary of the
-    same workload and kernel instance (profiles/r*_<workload>_pmc.json, tools/profile_round.sh +
-    tools/pmc_summary.py; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM), or None."""
+    same workload and kernel instance (profiles/r*_<workload>[_<tag>]_pmc.json,
+    tools/profile_round.sh + tools/pmc_summary.py; FETCH_SIZE doubled per MI355X_MICROARCH.md
+    §HBM), or None. `compute` is part of the kernel instance only through `variant`."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_pmc.json")))
-    if not files or not (300 <= variant < 600):
+    files = glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_pmc.json")) + \
+        glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_*_pmc.json"))
+    if not files or not (300 <= variant < 700):
         return None, None
     g = {"logistic": 0, "least_squares": 1, "hinge": 2}[grad]
     sname = "float" if storage == "f32" else "double"
-    if variant >= 500:
+    if variant >= 600:
+        prefix = f"psgd::chain_sparse_lds<{sname}, {g}, 0>"
+    elif variant >= 500:
         prefix = f"psgd::chain_block64<{sname}, {g}, 0, {variant - 500},"
     elif variant >= 410:
         prefix = f"psgd::chain_sparse_spec<{sname}, {g}, 0>"
@@ -60,13 +67,15 @@ def pmc_traffic(workload, grad, variant, storage, rows):
         prefix = f"psgd::chain_sparse<{sname}, {g}, 0>"
     else:
         prefix = f"psgd::chain_block<{sname}, {g}, 0, {variant - 300},"
-    with open(files[-1]) as f:
-        summ = json.load(f)
-    for name, e in summ.get("kernels", {}).items():
-        if name.startswith(prefix) and "hbm_bytes" in e:
-            # the summary's launch may have processed a different row count (--rows): per row
-            per_row = e["hbm_bytes"] / max(summ.get("rows_per_launch") or rows, 1)
-            return per_row * rows, os.path.relpath(files[-1], ROOT)
+    # newest round first (r02 before r01), then the file name
+    for path in sorted(files, key=lambda f: os.path.basename(f), reverse=True):
+        with open(path) as f:
+            summ = json.load(f)
+        for name, e in summ.get("kernels", {}).items():
+            if name.startswith(prefix) and "hbm_bytes" in e:
+                # the summary's launch may have processed a different row count (--rows): per row
+                per_row = e["hbm_bytes"] / max(summ.get("rows_per_launch") or rows, 1)
+                return per_row * rows, os.path.relpath(path, ROOT)
     return None, None
 
 
@@ -97,6 +106,8 @@ def parse():
                     help="miniBatchFraction: batch i = RDD.sample(false, f, 42 + i) per partition")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--secondary", default=DEFAULT_SECONDARY,
+                    help="comma list of workload[:compute] measured after the headline (1 GPU only; '' = none)")
     ap.add_argument("--prewarm-s", type=float, default=1.0,
                     help="untimed epochs for this long before the warmup steps (GPU clock ramp)")
     return ap.parse_args()
@@ -205,6 +216,150 @@ def cpu_baseline(grad, d, P, step, budget_s, seed=7, csr_nnz=0):
                       f"{epochs} epochs, {cores} threads, {dt:.1f} s"}
 
 
+def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, rows, fraction,
+                 steps, warmup, prewarm_s):
+    """One workload: synthetic shard in HBM, prewarm, W warmup steps, K timed steps (barrier +
+    synchronize on both sides, max over ranks). Returns the measurement as a dict."""
+    import numpy as np
+    grad, n, d, P, step, sdt, cfg_name = WORKLOADS[workload]
+    if rows:
+        n = rows
+    csr = workload in CSR_NNZ
+    if csr:
+        rp, col, val, y, offs = make_csr_shard(torch, dev, n, d, P, grad, sdt, 1000 + rank,
+                                               CSR_NNZ[workload])
+        torch.cuda.synchronize()
+        parts = [pkg.DeviceCsrPartition(y[a:b], rp[a:b + 1], col, val, d) for a, b in zip(offs[:-1], offs[1:])]
+        empty = lambda: pkg.DeviceCsrPartition(y[:0], rp[:1], col, val, d)
+    else:
+        X, y, offs = make_shard(torch, dev, n, d, P, grad, sdt, 1000 + rank)
+        torch.cuda.synchronize()
+        parts = [pkg.DevicePartition(y[a:b], X[a:b], d) for a, b in zip(offs[:-1], offs[1:])]
+        empty = lambda: pkg.DevicePartition(y[:0], X[:0], d)
+    # global partition list: this rank's block is [rank*P, (rank+1)*P)
+    all_parts = [None] * (P * world)
+    all_parts[rank * P:(rank + 1) * P] = parts
+    for i in range(len(all_parts)):
+        if all_parts[i] is None:
+            all_parts[i] = empty()  # placeholders for other ranks
+    data = pkg.PartitionedData(all_parts)
+    engine = pkg.HipEngine(data, rank, world, device=local)
+    gcls = {"least_squares": pkg.LeastSquaresGradient, "logistic": pkg.LogisticGradient,
+            "hinge": pkg.HingeGradient}[grad]()
+    reg = REG.get(workload, 0.0)
+    ucls = pkg.SquaredL2SGDUpdater() if reg > 0 else pkg.SimpleSGDUpdater()
+    params = pkg.make_params(gcls, ucls, step, reg, fraction, 0.0, compute)
+    w = engine.weights(np.zeros(d))
+    stream = engine.stream  # the engine's kernels and copies all run on this stream
+
+    def one_step(w, it, ev=None):
+        params.iteration = it
+        if ev is not None:
+            ev[0].record(stream)
+        folded, _ = engine.epoch(params, w)
+        if ev is not None:
+            ev[1].record(stream)
+        rv, loss, cnt = engine.scalars(folded)  # D2H of the 3 driver scalars (PSGD:278-287)
+        if ev is not None:
+            kernel_ms.append(engine.ctx.last_chain_ms())  # HIP events around the chain launch
+        return (engine.adopt(folded) if cnt > 0 else w), cnt, loss
+
+    kernel_ms = []
+
+    # Device prewarm (part of setup, like data generation): the chain kernel's first launches run
+    # below steady-state clocks (rocprof trace: 3.5-3.8 ms for the first c2 epochs, 3.1 ms from
+    # the sixth on), so untimed epochs run for --prewarm-s seconds before the W warmup steps.
+    # The model they produce is discarded: the warmup and timed steps start from w = 0.
+    # Every epoch holds a collective when N > 1, so all ranks run the same count: two epochs
+    # time one, and the count for --prewarm-s is the max over ranks.
+    w0 = w
+    prewarm_epochs = 0
+    if prewarm_s > 0:
+        wp = w0
+        torch.cuda.synchronize()
+        t_pw = time.perf_counter()
+        for _ in range(2):
+            wp, _, _ = one_step(wp, prewarm_epochs + 1)
+            prewarm_epochs += 1
+        torch.cuda.synchronize()
+        per_epoch = (time.perf_counter() - t_pw) / 2
+        want = max(2, min(5000, int(prewarm_s / max(per_epoch, 1e-6))))
+        if world > 1:
+            t = torch.tensor([want], dtype=torch.int64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            want = int(t.item())
+        while prewarm_epochs < want:
+            wp, _, _ = one_step(wp, prewarm_epochs + 1)
+            prewarm_epochs += 1
+        torch.cuda.synchronize()
+        kernel_ms.clear()
+    w = w0
+    for i in range(warmup):
+        w, cnt, loss = one_step(w, i + 1)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(steps)]
+    t0 = time.perf_counter()
+    total = 0
+    for i in range(steps):
+        w, cnt, loss = one_step(w, warmup + i + 1, events[i])
+        total += cnt
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    # `cnt` is the whole job's sample count of the step (the fold sums counts over all ranks)
+    samples_per_step = cnt
+    if fraction >= 1.0:
+        assert samples_per_step == n * world, (samples_per_step, n * world)
+    else:  # sampled batches differ per step: the timed steps' samples
+        samples_per_step = total / steps
+    value = samples_per_step * steps / elapsed
+    assert np.isfinite(loss), loss
+    epoch_ms = [a.elapsed_time(b) for a, b in events]
+    avg_epoch_s = sum(epoch_ms) / len(epoch_ms) / 1e3
+    avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+    es = 4 if sdt == "f32" else 8
+    if csr:  # values + int32 columns + int64 row pointer + f64 label (weights: L2/MALL-resident)
+        bytes_per_sample = CSR_NNZ[workload] * (es + 4) + 8 + 8
+    else:
+        bytes_per_sample = (d + 1) * es  # row + label (SURVEY §8d; weights are on chip)
+    local_samples = n if fraction >= 1.0 else samples_per_step / world
+    # one chain-kernel launch processes every (sampled) row of this GPU's partitions
+    achieved = local_samples * bytes_per_sample / avg_kernel_s / 1e9
+    variant = engine.ctx.last_kernel()
+    traffic, traffic_src = pmc_traffic(workload, grad, variant, sdt, n, compute)
+    res = {
+        "value": value, "ms_per_step": elapsed / steps * 1e3, "dtype": compute, "loss": loss,
+        "config": {"workload": f"{workload}: {cfg_name}", "rows_per_gpu": n, "d": d,
+                   "chains_per_gpu": P, "storage": sdt, "gradient": grad,
+                   "updater": "squared_l2" if reg > 0 else "simple", "reg_param": reg,
+                   "step_size": step, "convergence_tol": 0.0, "mini_batch_fraction": fraction,
+                   "parallelism": f"dp{world} (chains sharded, RCCL all-gather + fold per epoch)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": traffic_src,
+                     "kernel": kernel_name(variant),
+                     "bytes_per_launch": local_samples * bytes_per_sample,
+                     "bytes_per_sample": bytes_per_sample, "avg_kernel_ms": avg_kernel_s * 1e3,
+                     "avg_epoch_ms": avg_epoch_s * 1e3,
+                     "timing": "HIP events recorded around each chain-kernel launch on its stream"},
+        "prewarm": {"seconds": prewarm_s, "epochs": prewarm_epochs,
+                    "note": "untimed epochs before the warmup steps (GPU clock ramp); their model is discarded"},
+        "_meta": (grad, d, P, step, csr),
+    }
+    del engine, data, parts, all_parts
+    return res
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
@@ -236,147 +391,36 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    grad, n, d, P, step, sdt, cfg_name = WORKLOADS[args.workload]
-    if args.rows:
-        n = args.rows
-    csr = args.workload in CSR_NNZ
-    if csr:
-        rp, col, val, y, offs = make_csr_shard(torch, dev, n, d, P, grad, sdt, 1000 + rank,
-                                               CSR_NNZ[args.workload])
-        torch.cuda.synchronize()
-        parts = [pkg.DeviceCsrPartition(y[a:b], rp[a:b + 1], col, val, d) for a, b in zip(offs[:-1], offs[1:])]
-        empty = lambda: pkg.DeviceCsrPartition(y[:0], rp[:1], col, val, d)
-    else:
-        X, y, offs = make_shard(torch, dev, n, d, P, grad, sdt, 1000 + rank)
-        torch.cuda.synchronize()
-        parts = [pkg.DevicePartition(y[a:b], X[a:b], d) for a, b in zip(offs[:-1], offs[1:])]
-        empty = lambda: pkg.DevicePartition(y[:0], X[:0], d)
-    # global partition list: this rank's block is [rank*P, (rank+1)*P)
-    all_parts = [None] * (P * world)
-    all_parts[rank * P:(rank + 1) * P] = parts
-    for i in range(len(all_parts)):
-        if all_parts[i] is None:
-            all_parts[i] = empty()  # placeholders for other ranks
-    data = pkg.PartitionedData(all_parts)
-    engine = pkg.HipEngine(data, rank, world, device=local)
-    gcls = {"least_squares": pkg.LeastSquaresGradient, "logistic": pkg.LogisticGradient,
-            "hinge": pkg.HingeGradient}[grad]()
-    reg = REG.get(args.workload, 0.0)
-    ucls = pkg.SquaredL2SGDUpdater() if reg > 0 else pkg.SimpleSGDUpdater()
-    params = pkg.make_params(gcls, ucls, step, reg, args.fraction, 0.0, args.compute)
-    import numpy as np
-    w = engine.weights(np.zeros(d))
-    stream = engine.stream  # the engine's kernels and copies all run on this stream
-
-    def one_step(w, it, ev=None):
-        params.iteration = it
-        if ev is not None:
-            ev[0].record(stream)
-        folded, _ = engine.epoch(params, w)
-        if ev is not None:
-            ev[1].record(stream)
-        rv, loss, cnt = engine.scalars(folded)  # D2H of the 3 driver scalars (PSGD:278-287)
-        if ev is not None:
-            kernel_ms.append(engine.ctx.last_chain_ms())  # HIP events around the chain launch
-        return (engine.adopt(folded) if cnt > 0 else w), cnt, loss
-
-    kernel_ms = []
-
-    # Device prewarm (part of setup, like data generation): the chain kernel's first launches run
-    # below steady-state clocks (rocprof trace: 3.5-3.8 ms for the first c2 epochs, 3.1 ms from
-    # the sixth on), so untimed epochs run for --prewarm-s seconds before the W warmup steps.
-    # The model they produce is discarded: the warmup and timed steps start from w = 0.
-    # Every epoch holds a collective when N > 1, so all ranks run the same count: two epochs
-    # time one, and the count for --prewarm-s is the max over ranks.
-    w0 = w
-    prewarm_epochs = 0
-    if args.prewarm_s > 0:
-        wp = w0
-        torch.cuda.synchronize()
-        t_pw = time.perf_counter()
-        for _ in range(2):
-            wp, _, _ = one_step(wp, prewarm_epochs + 1)
-            prewarm_epochs += 1
-        torch.cuda.synchronize()
-        per_epoch = (time.perf_counter() - t_pw) / 2
-        want = max(2, min(5000, int(args.prewarm_s / max(per_epoch, 1e-6))))
-        if world > 1:
-            t = torch.tensor([want], dtype=torch.int64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            want = int(t.item())
-        while prewarm_epochs < want:
-            wp, _, _ = one_step(wp, prewarm_epochs + 1)
-            prewarm_epochs += 1
-        torch.cuda.synchronize()
-        kernel_ms.clear()
-    w = w0
-    for i in range(args.warmup):
-        w, cnt, loss = one_step(w, i + 1)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    total = 0
-    for i in range(args.steps):
-        w, cnt, loss = one_step(w, args.warmup + i + 1, events[i])
-        total += cnt
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    # `cnt` is the whole job's sample count of the step (the fold sums counts over all ranks)
-    samples_per_step = cnt
-    if args.fraction >= 1.0:
-        assert samples_per_step == n * world, (samples_per_step, n * world)
-    else:  # sampled batches differ per step: the timed steps' samples
-        samples_per_step = total / args.steps
-    value = samples_per_step * args.steps / elapsed
-    assert np.isfinite(loss), loss
-    epoch_ms = [a.elapsed_time(b) for a, b in events]
-    avg_epoch_s = sum(epoch_ms) / len(epoch_ms) / 1e3
-    avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
-    es = 4 if sdt == "f32" else 8
-    if csr:  # values + int32 columns + int64 row pointer + f64 label (weights: L2/MALL-resident)
-        bytes_per_sample = CSR_NNZ[args.workload] * (es + 4) + 8 + 8
-    else:
-        bytes_per_sample = (d + 1) * es  # row + label (weights are on chip)
-    local_samples = n if args.fraction >= 1.0 else samples_per_step / world
-    # one chain-kernel launch processes every (sampled) row of this GPU's partitions
-    achieved = local_samples * bytes_per_sample / avg_kernel_s / 1e9
-    traffic, traffic_src = pmc_traffic(args.workload, grad, engine.ctx.last_kernel(), sdt, n)
+    res = run_workload(torch, dist, pkg, dev, rank, world, local, args.workload, args.compute,
+                       args.rows, args.fraction, args.steps, args.warmup, args.prewarm_s)
+    grad, d, P, step, csr = res.pop("_meta")
+    res.pop("loss")
     out = {
         "metric": "training samples/sec (whole node) + achieved HBM GB/s, logistic SGD 1/2/4/8 GPUs",
-        "value": value, "unit": "samples/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "value": res["value"], "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": res["ms_per_step"],
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": args.compute, "data": "synthetic (device-generated, resident in HBM)",
-        "config": {"workload": f"{args.workload}: {cfg_name}", "rows_per_gpu": n, "d": d,
-                   "chains_per_gpu": P, "storage": sdt, "gradient": grad,
-                   "updater": "squared_l2" if reg > 0 else "simple", "reg_param": reg,
-                   "step_size": step, "convergence_tol": 0.0, "mini_batch_fraction": args.fraction,
-                   "parallelism": f"dp{world} (chains sharded, RCCL all-gather + fold per epoch)"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_source": traffic_src,
-                     "kernel": kernel_name(engine.ctx.last_kernel()),
-                     "bytes_per_launch": local_samples * bytes_per_sample,
-                     "bytes_per_sample": bytes_per_sample, "avg_kernel_ms": avg_kernel_s * 1e3,
-                     "avg_epoch_ms": avg_epoch_s * 1e3,
-                     "timing": "HIP events recorded around each chain-kernel launch on its stream"},
-        "prewarm": {"seconds": args.prewarm_s, "epochs": prewarm_epochs,
-                    "note": "untimed epochs before the warmup steps (GPU clock ramp); their model is discarded"},
+        "dtype": res["dtype"], "data": "synthetic (device-generated, resident in HBM)",
+        "config": res["config"], "roofline": res["roofline"], "prewarm": res["prewarm"],
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(grad, d, P, step, args.cpu_seconds,
                                            csr_nnz=CSR_NNZ[args.workload] if csr else 0)
+    # Secondary lines (one GPU only): the other BASELINE configs' per-GPU workloads under the
+    # same clock, each with its own roofline (VERDICT r01 "let the driver observe" them).
+    secondary = [s for s in args.secondary.split(",") if s] if world == 1 else []
+    if secondary:
+        out["secondary"] = []
+    for spec in secondary:
+        wl, _, comp = spec.partition(":")
+        torch.cuda.empty_cache()
+        r = run_workload(torch, dist, pkg, dev, rank, world, local, wl, comp or "f32",
+                         SECONDARY_ROWS.get(wl, 0), 1.0, args.steps, args.warmup,
+                         min(args.prewarm_s, 0.5))
+        r.pop("_meta")
+        r["samples_per_s"] = r.pop("value")
+        r["loss"] = float(r["loss"])
+        out["secondary"].append(r)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -7,8 +7,9 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/prof
-ARGS=${BENCH_ARGS:-"--no-cpu-baseline"}   # the bench defaults (5 timed steps, 2 warmup)
+OUT=${PROF_OUT:-gpurun_out/prof}
+# the bench defaults (5 timed steps, 2 warmup), headline workload only (no secondary lines)
+ARGS="--secondary= ${BENCH_ARGS:---no-cpu-baseline}"
 mkdir -p $OUT
 # one rank only: bench.py --gpus N > 1 would start a launcher under the profiler
 case " $ARGS " in *" --gpus "[2-9]*|*" --gpus="[2-9]*) echo "profile a single rank (--gpus 1)"; exit 2;; esac
