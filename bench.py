@@ -84,6 +84,9 @@ def kernel_name(variant):
         return f"chain_block (NV={variant - 300}: blocked fp32 chain, 8-row Gram blocks)"
     if 500 <= variant < 600:
         return f"chain_block64 (NV={variant - 500}: blocked fp64 chain, 8-row Gram blocks)"
+    if 600 <= variant < 700:
+        return (f"chain_sparse_lds (fp32 CSR chain, weights LDS-resident [tail past ~160 KiB: L2-resident, "
+                f"gathered {8 if variant >= 610 else 4} samples ahead with an LDS feature-tag correction])")
     if 410 <= variant < 500:
         return ("chain_sparse_spec (fp32 CSR chain, weights L2/MALL-resident, gathers 8 samples "
                 "ahead with an LDS feature-tag correction)")
@@ -102,6 +105,7 @@ def parse():
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--compute", default="f32", choices=["f32", "f64"])
     ap.add_argument("--rows", type=int, default=0, help="override rows per GPU (testing)")
+    ap.add_argument("--features", type=int, default=0, help="override d (experiments; not a BASELINE config)")
     ap.add_argument("--fraction", type=float, default=1.0,
                     help="miniBatchFraction: batch i = RDD.sample(false, f, 42 + i) per partition")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
@@ -217,13 +221,16 @@ def cpu_baseline(grad, d, P, step, budget_s, seed=7, csr_nnz=0):
 
 
 def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, rows, fraction,
-                 steps, warmup, prewarm_s):
+                 steps, warmup, prewarm_s, features=0):
     """One workload: synthetic shard in HBM, prewarm, W warmup steps, K timed steps (barrier +
     synchronize on both sides, max over ranks). Returns the measurement as a dict."""
     import numpy as np
     grad, n, d, P, step, sdt, cfg_name = WORKLOADS[workload]
     if rows:
         n = rows
+    if features:
+        d = features
+        cfg_name += f" [d overridden: {d}]"
     csr = workload in CSR_NNZ
     if csr:
         rp, col, val, y, offs = make_csr_shard(torch, dev, n, d, P, grad, sdt, 1000 + rank,
@@ -392,7 +399,7 @@ def main():
     torch.cuda.set_device(dev)
 
     res = run_workload(torch, dist, pkg, dev, rank, world, local, args.workload, args.compute,
-                       args.rows, args.fraction, args.steps, args.warmup, args.prewarm_s)
+                       args.rows, args.fraction, args.steps, args.warmup, args.prewarm_s, args.features)
     grad, d, P, step, csr = res.pop("_meta")
     res.pop("loss")
     out = {

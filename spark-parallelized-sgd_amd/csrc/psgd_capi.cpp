@@ -624,8 +624,8 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         return e && *e && *e != '0';
     }();
     if (want_stamps && layout == psgd::kCsr) {
-        HIP_TRY(ctx->stamps.ensure((size_t)P * 4 * sizeof(unsigned long long)));
-        HIP_TRY(hipMemsetAsync(ctx->stamps.p, 0, (size_t)P * 4 * sizeof(unsigned long long), st));
+        HIP_TRY(ctx->stamps.ensure((size_t)P * 6 * sizeof(unsigned long long)));
+        HIP_TRY(hipMemsetAsync(ctx->stamps.p, 0, (size_t)P * 6 * sizeof(unsigned long long), st));
         L.stamps = ctx->stamps.as<unsigned long long>();
     }
     L.zbuf = nullptr;
@@ -634,9 +634,9 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
     L.wf32 = nullptr;
     L.wstride = 0;
     if (layout == psgd::kCsr && params->compute_dtype == PSGD_F32) {
-        // fp32 working weights of the CSR kernel (one d-vector per chain, HBM/L2-resident, and
-        // 128 floats the kernel's masked-off lanes load from / store to)
-        L.wstride = (int64_t)d + 128;
+        // fp32 working weights of the CSR kernels (one d-vector per chain, HBM/L2-resident, and
+        // 128 + 1024 floats the kernels' masked-off lanes load from / store to)
+        L.wstride = (int64_t)d + 128 + 1024;
         HIP_TRY(ctx->wf32.ensure((size_t)P * (size_t)L.wstride * sizeof(float)));
         L.wf32 = ctx->wf32.as<float>();
     }
@@ -686,17 +686,22 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
                                     lds_spread_bytes(ctx, (size_t)P), st, &ctx->last_variant, max_nnz);
         HIP_TRY(hipEventRecord(ctx->ev_end, st));
         ctx->ev_recorded = (e == 0);
-        if (L.stamps) {   // PSGD_STAMPS=1: per-chain cycle counters of the CSR fp32 kernel (stderr)
-            std::vector<unsigned long long> h((size_t)P * 4);
+        if (L.stamps) {   // PSGD_STAMPS=1: per-chain cycle counters of the CSR fp32 kernels (stderr)
+            // chain_sparse_lds: {chain, loader, tagger} x {total, waiting}; chain_sparse_spec:
+            // {chain, helper} x {total, waiting}
+            const int K6 = ctx->last_variant >= 600 ? 6 : 4;
+            std::vector<unsigned long long> h((size_t)P * 6);
             HIP_TRY(hipMemcpyAsync(h.data(), L.stamps, h.size() * 8, hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
-            std::vector<double> v[4];
+            std::vector<double> v[6];
             for (int p = 0; p < P; ++p)
-                for (int k = 0; k < 4; ++k) v[k].push_back((double)h[(size_t)p * 4 + k] / std::max<int64_t>(n_max, 1));
-            const char* names[4] = {"chain.total", "chain.wait_ready", "helper.total", "helper.wait_done"};
-            for (int k = 0; k < 4; ++k) {
+                for (int k = 0; k < K6; ++k)
+                    v[k].push_back((double)h[(size_t)p * (ctx->last_variant >= 600 ? 6 : 4) + k] / std::max<int64_t>(n_max, 1));
+            const char* n4[4] = {"chain.total", "chain.wait", "helper.total", "helper.wait"};
+            const char* n6[6] = {"chain.total", "chain.wait", "loader.total", "loader.wait", "tagger.total", "tagger.wait"};
+            for (int k = 0; k < K6; ++k) {
                 std::sort(v[k].begin(), v[k].end());
-                fprintf(stderr, "psgd stamps %-18s cycles/row median %8.1f\n", names[k], v[k][v[k].size() / 2]);
+                fprintf(stderr, "psgd stamps %-18s cycles/row median %8.1f\n", K6 == 6 ? n6[k] : n4[k], v[k][v[k].size() / 2]);
             }
         }
         if (e == -2) return fail(PSGD_EUNSUPPORTED, "this gradient/updater/layout combination is not built");

@@ -187,6 +187,42 @@ __device__ __forceinline__ T gradient_scalar(T z, T y, T& mult) {
     }
 }
 
+// fp32 CSR chains (psgd_sparse*.hip): the sample's update coefficient c = -s * mult (the row's
+// new weights are w_j + c x_j) and its loss, in fp32 (LeastSquares loss is halved by the caller).
+template <int GRAD>
+__device__ __forceinline__ float sparse_coef(float z, float y, float s, float& loss) {
+    if constexpr (GRAD == G_LEAST_SQUARES) {
+        const float diff = z - y;
+        loss = diff * diff;                      // halved once at the end
+        return -s * diff;
+    } else if constexpr (GRAD == G_LOGISTIC) {
+        const float margin = -z;
+        const float e = __expf(margin);
+        const float sig = __builtin_amdgcn_rcpf(1.0f + e);
+        const float ax = __builtin_fabsf(margin);
+        const float l = __logf(1.0f + __expf(-ax)) + (margin > 0.0f ? margin : 0.0f);
+        loss = y > 0.0f ? l : l - margin;
+        return -s * (sig - y);
+    } else {
+        const float ls = 2.0f * y - 1.0f;
+        const float lz = ls * z;
+        const bool on = 1.0f > lz;
+        loss = on ? 1.0f - lz : 0.0f;
+        return on ? s * ls : 0.0f;
+    }
+}
+
+// fp32 CSR chains: the chain's VMEM instructions are inline asm: their count per sample is what its vmcnt waits
+// rely on, so the compiler must neither merge nor drop any of them.
+__device__ __forceinline__ float gather_sc1(const float* p) {
+    float v;
+    asm volatile("global_load_dword %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ void store_f32(float* p, float v) {
+    asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");
+}
+
 template <int... Is, typename F>
 __device__ __forceinline__ void static_for_impl(std::integer_sequence<int, Is...>, F&& f) {
     (f(std::integral_constant<int, Is>{}), ...);

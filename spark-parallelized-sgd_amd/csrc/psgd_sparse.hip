@@ -24,31 +24,9 @@
 #include "psgd_device.h"
 
 #include <stdlib.h>
+#include <string.h>
 
 namespace psgd {
-
-template <int GRAD>
-__device__ __forceinline__ float sparse_coef(float z, float y, float s, float& loss) {
-    if constexpr (GRAD == G_LEAST_SQUARES) {
-        const float diff = z - y;
-        loss = diff * diff;                      // halved once at the end
-        return -s * diff;
-    } else if constexpr (GRAD == G_LOGISTIC) {
-        const float margin = -z;
-        const float e = __expf(margin);
-        const float sig = __builtin_amdgcn_rcpf(1.0f + e);
-        const float ax = __builtin_fabsf(margin);
-        const float l = __logf(1.0f + __expf(-ax)) + (margin > 0.0f ? margin : 0.0f);
-        loss = y > 0.0f ? l : l - margin;
-        return -s * (sig - y);
-    } else {
-        const float ls = 2.0f * y - 1.0f;
-        const float lz = ls * z;
-        const bool on = 1.0f > lz;
-        loss = on ? 1.0f - lz : 0.0f;
-        return on ? s * ls : 0.0f;
-    }
-}
 
 template <typename S, int GRAD, int UPD>
 __global__ __launch_bounds__(64) void chain_sparse(ChainLaunch L, KParams kp) {
@@ -224,17 +202,6 @@ struct SpecSlot {
     int32_t pad;
     double y, s;
 };
-
-// The chain's VMEM instructions are inline asm: their count per sample is what its vmcnt waits
-// rely on, so the compiler must neither merge nor drop any of them.
-__device__ __forceinline__ float gather_sc1(const float* p) {
-    float v;
-    asm volatile("global_load_dword %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
-    return v;
-}
-__device__ __forceinline__ void store_f32(float* p, float v) {
-    asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");
-}
 
 template <typename S, int GRAD, int UPD>
 __global__ __launch_bounds__(128) void chain_sparse_spec(ChainLaunch L, KParams kp) {
@@ -604,10 +571,18 @@ int launch_sparse_chains(const ChainLaunch& L, const KParams& kp, int storage, i
                          int updater, int64_t max_nnz, hipStream_t stream, int* kernel_variant) {
     if (kp.n_chains <= 0) return 0;
     if (!L.wf32 || L.wstride < (int64_t)kp.d + 128) return (int)hipErrorInvalidValue;
-    static const bool no_spec = [] {
-        const char* e = getenv("PSGD_SPARSE_NOSPEC");   // A/B measurements
-        return e && *e && *e != '0';
-    }();
+    // PSGD_SPARSE_KERNEL = lds | spec | plain forces a variant (tests, A/B measurements; read
+    // at every launch); default: the first that applies in that order
+    const char* force = getenv("PSGD_SPARSE_KERNEL");
+    const bool any = !force || !*force;
+    const bool no_lds = !any && strcmp(force, "lds") != 0;
+    const bool no_spec = !any && strcmp(force, "spec") != 0;
+    // first choice: the chain's weights in LDS (psgd_sparse_lds.hip), for rows of <= 128
+    // non-zeros and d up to ~65k features
+    if (!no_lds) {
+        const int rc = launch_sparse_lds_chains(L, kp, storage, gradient, updater, max_nnz, stream, kernel_variant);
+        if (rc != -3) return rc;
+    }
     const size_t lds = sparse_spec_lds_bytes(kp.d);
     if (!no_spec && max_nnz <= SCAP && lds <= 160 * 1024) {
         if (kernel_variant) *kernel_variant = 410 + storage;

@@ -1,0 +1,616 @@
+// psgd_sparse_lds.hip -- the fp32 CSR chain with the chain's weights resident in LDS (gfx950).
+//
+// Reference: ParallelizedSGD.scala:243-270 (the chain: weights read by Gradient.compute at :254,
+// written by SGDUpdater.compute at :255-256), [ext] MLlib 1.6.1 Gradient.scala on SparseVector rows
+// (the gradient is mult * x, non-zero only at the row's indices), SGDUpdater.scala:86-98 (Simple)
+// and :163-181 (SquaredL2, alpha-scaled lazy form as in psgd_sparse.hip).
+//
+// One workgroup = one chain = one CU (the 160 KiB LDS holds one chain's weights). Features
+// [0, K) live in LDS as fp32 ("head"); when d does not fit, features [K, d) ("tail") stay in the
+// chain's fp32 vector in HBM (L.wf32), 4 (d - K) bytes per chain instead of 4 d -- at rcv1 shape
+// (d = 47,236) ~100 KB, so 32 chains per XCD fit its 4 MiB L2 where whole vectors did not.
+//   * head entries: the chain reads w_j from LDS at the sample and writes the new value back
+//     (one wave's LDS operations execute in program order, so row t+1 reads row t's update);
+//   * tail entries: gathered from HBM SK samples ahead (sc1 loads: L2 sees this wave's earlier
+//     stores first) and corrected as in chain_sparse_spec: a per-feature tag table over the tail
+//     (2 B per tail feature: (row & 255) << 8 | entry of the latest row holding the feature)
+//     names the latest of the SK preceding rows with the same feature, whose new value the chain
+//     left in that row's LDS slot in place of x_j. Tags never alias: the tagger sweeps 1/128 of
+//     the table per row and clears tags older than SK rows, so no tag outlives 256 rows.
+// Three waves, one per SIMD, each a short branch-free loop:
+//   wave 0 (chain)  per sample t: one LDS read per entry (head: W[j]; corrected tail: the earlier
+//                   row's slot; else the gathered value), dot + wave reduction + coefficient, one
+//                   LDS write per entry, the gathers of row t + SK and the row's tail stores
+//                   (fixed 2 + 2 VMEM instructions: s_waitcnt vmcnt(4 SK) finds row t's gather);
+//                   the next sample's slot data is read under the current sample's LDS latency;
+//   wave 1 (loader) the partition's CSR entries into an SR-slot LDS ring (16 rows of loads in
+//                   flight in registers, 8-row groups), labels / steps / nnz into a 128-row meta
+//                   ring, 64 rows per batch;
+//   wave 2 (tagger) per row: sweep a tag chunk, tail tag lookups + updates, and each entry's LDS
+//                   read/write addresses (rw) into the slot.
+// Rows are published through LDS counters: loaded (loader), tagged (tagger), done (chain).
+// No MFMA: the work per sample is a ~100-long gather-dot and scatter.
+#include "psgd_device.h"
+
+#include <stdlib.h>
+
+namespace psgd {
+
+constexpr int LCAP = 128;                  // entries per row (two per lane)
+
+// The lanes of `pred`, plus lane 63.
+__device__ __forceinline__ uint64_t ballot_or63(bool pred) {
+    return __builtin_amdgcn_ballot_w64(pred) | (1ull << 63);
+}
+// gather_sc1 / store_f32 (psgd_device.h) under an explicit EXEC mask; lanes outside `mask` keep
+// their destination register as it was.
+__device__ __forceinline__ float gather_sc1_masked(const float* p, uint64_t mask) {
+    float v;
+    uint64_t saved;
+    asm volatile(
+        "s_mov_b64 %1, exec\n\t"
+        "s_mov_b64 exec, %3\n\t"
+        "global_load_dword %0, %2, off sc1\n\t"
+        "s_mov_b64 exec, %1"
+        : "=&v"(v), "=&s"(saved) : "v"(p), "s"(mask) : "memory");
+    return v;
+}
+__device__ __forceinline__ void store_f32_masked(float* p, float v, uint64_t mask) {
+    uint64_t saved;
+    asm volatile(
+        "s_mov_b64 %0, exec\n\t"
+        "s_mov_b64 exec, %3\n\t"
+        "global_store_dword %1, %2, off\n\t"
+        "s_mov_b64 exec, %0"
+        : "=&s"(saved) : "v"(p), "v"(v), "s"(mask) : "memory");
+}
+constexpr int kMetaRing = 128;             // rows of label / step / nnz
+constexpr int kSweepRows = 128;            // the tag table is swept once per this many rows
+constexpr int64_t kLdsCap = 160 * 1024;    // LDS per CU (gfx950)
+
+template <int SK>
+struct LdsRing {
+    // the chain needs rows up to t + SK + 1 staged at sample t (done = t); the loader reuses the
+    // slot of row u - SR once the chain is done with row u - SR + SK (its new values are read by
+    // the SK rows after it): progress needs t + SK + 1 - SR + SK + 1 <= t
+    static constexpr int SR = 2 * SK + 8 <= 16 ? 16 : 32;
+    static_assert(SR >= 2 * SK + 2, "ring too small for the speculation depth");
+};
+
+struct LdsHeader {
+    unsigned loaded;   // rows whose entries are in their slots (loader)
+    unsigned tagged;   // rows whose LDS addresses are in their slots (tagger)
+    unsigned done;     // rows finished by the chain
+    unsigned stop;
+    unsigned dummy;    // target of inactive lanes' LDS weight reads and writes
+    unsigned dtag;     // target of inactive lanes' tag reads and writes
+    unsigned pad[2];
+};
+struct LdsMeta {
+    float y[kMetaRing];
+    float s[kMetaRing];       // stepSize / sqrt(j), rounded (fp32 compute)
+    double s64[kMetaRing];    // the same in f64 (SquaredL2's alpha)
+    int32_t nnz[kMetaRing];
+};
+struct LdsSlot {
+    int32_t col[LCAP];   // feature index
+    float val[LCAP];     // x_j; the chain replaces a tail entry's x_j by its new weight
+    uint32_t rw[LCAP];   // LDS dword addresses: read (bits 0-15), write (bits 16-31)
+};
+constexpr unsigned kLdsDummy = 4;              // dword index of LdsHeader::dummy
+constexpr int64_t kMetaOff = sizeof(LdsHeader);
+constexpr int64_t kSlotOff = kMetaOff + sizeof(LdsMeta);
+static_assert(kSlotOff % 16 == 0 && sizeof(LdsSlot) % 16 == 0, "alignment");
+
+template <int SK>
+constexpr int64_t lds_fixed_bytes() { return kSlotOff + LdsRing<SK>::SR * (int64_t)sizeof(LdsSlot); }
+// tail tag table entries (u16), rounded for the sweep's 4-tag accesses
+__host__ __device__ inline int64_t tag_entries(int64_t d, int64_t K) { return ((d - K) + 3) & ~int64_t(3); }
+template <int SK>
+int64_t lds_bytes(int64_t d, int64_t K) { return lds_fixed_bytes<SK>() + 4 * K + 2 * tag_entries(d, K); }
+// Features [0, K) in LDS: all of them when they fit, else as many as leave room for the tail's
+// tag table (K a multiple of 4: the table stays 8-byte aligned); -1 when not even the table fits.
+template <int SK>
+int64_t lds_head(int64_t d) {
+    const int64_t budget = kLdsCap - lds_fixed_bytes<SK>();
+    if (4 * d <= budget) return d;
+    int64_t K = (budget - 2 * (d + 4)) / 2;
+    K &= ~int64_t(3);
+    return K >= 0 ? K : -1;
+}
+
+// TAIL = false: every feature is in LDS (K = d), the chain issues no VMEM at all.
+template <typename S, int GRAD, int UPD, int SK, bool TAIL>
+__global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams kp, int K) {
+    constexpr bool L2 = UPD == U_SQUARED_L2;
+    constexpr int SR = LdsRing<SK>::SR;
+    static_assert((SR & (SR - 1)) == 0, "slot index by mask");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    LdsHeader* hdr = reinterpret_cast<LdsHeader*>(smem);
+    LdsMeta* meta = reinterpret_cast<LdsMeta*>(smem + kMetaOff);
+    LdsSlot* slots = reinterpret_cast<LdsSlot*>(smem + kSlotOff);
+    float* lds = reinterpret_cast<float*>(smem);                 // dword-addressed view
+    constexpr unsigned kWoff = (unsigned)(lds_fixed_bytes<SK>() / 4);
+    float* W = lds + kWoff;                                      // head weights [K]
+    uint16_t* tagpos = reinterpret_cast<uint16_t*>(W + K);       // tail features K .. d-1
+    // dword index of val[0] of the slot holding row u
+    auto val_off = [](int64_t u) __attribute__((always_inline)) -> unsigned {
+        return (unsigned)((kSlotOff + (int64_t)(u & (SR - 1)) * (int64_t)sizeof(LdsSlot)) / 4) + LCAP;
+    };
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int chain = blockIdx.x;
+    const ChainDesc dsc = L.descs[chain];
+    const int d = kp.d;
+    const int64_t n = dsc.n_rows;
+    const int64_t T = tag_entries(d, K);
+    // The chain runs n_pad samples (a multiple of its unroll SK + 1) and reads up to row
+    // n_pad + SK ahead: the loader and the tagger stage n_fill rows, rows past n null (no
+    // entries, label and step 0), so no read in the chain needs a condition.
+    constexpr int GS = SK + 1;
+    const int64_t n_pad = (n + GS - 1) / GS * GS;
+    const int64_t n_fill = (n_pad + SK + 1 + 7) / 8 * 8;
+    // [d] (tail used) + [128] the loader's dummy sources + [1024] the chain's dummy targets
+    float* V = L.wf32 + (int64_t)chain * L.wstride;
+
+    for (int64_t i = threadIdx.x; i < T; i += blockDim.x) tagpos[i] = 0xFFFF;
+    for (int i = threadIdx.x; i < K; i += blockDim.x) W[i] = float(as_global(L.w_in)[i]);
+    if (threadIdx.x < 8) reinterpret_cast<unsigned*>(hdr)[threadIdx.x] = 0;
+    if (wave == 0) {
+        // the chain's tail gathers below are loads of these addresses from the same wave
+        for (int i = K + lane; i < d; i += 64) as_global_mut(V)[i] = float(as_global(L.w_in)[i]);
+    }
+    __syncthreads();
+
+    uint64_t st_wait = 0;                     // diagnostic (PSGD_STAMPS): cycles spent waiting
+    const uint64_t st_begin = __builtin_amdgcn_s_memtime();
+    // wait until *flag >= need (cached in `seen`); false when the chain stopped or the watchdog fired
+    auto wait_for = [&](unsigned& seen, const unsigned* flag, int64_t need, int code)
+        __attribute__((always_inline)) -> bool {
+        if ((int64_t)seen >= need) return true;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        const uint64_t c0 = __builtin_amdgcn_s_memtime();
+        for (;;) {
+            // relaxed: the flags and the data are LDS, which one wave writes in program order
+            seen = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if ((int64_t)seen >= need) {
+                __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                st_wait += __builtin_amdgcn_s_memtime() - c0;
+                return true;
+            }
+            if (__hip_atomic_load(&hdr->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kWatchdogTicks) {
+                __hip_atomic_fetch_or(L.watchdog, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                return false;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    };
+    auto publish = [&](unsigned* flag, int64_t v) __attribute__((always_inline)) {
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __hip_atomic_store(flag, (unsigned)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto stamp_out = [&](int k) __attribute__((always_inline)) {
+        if (L.stamps && lane == 0) {
+            L.stamps[(size_t)chain * 6 + 2 * k] = __builtin_amdgcn_s_memtime() - st_begin;
+            L.stamps[(size_t)chain * 6 + 2 * k + 1] = st_wait;
+        }
+    };
+
+    if (wave == 1) {
+        // ---------------- loader: entries into slots, labels / steps / nnz into the meta ring ----
+        const gptr<S> X = as_global(reinterpret_cast<const S*>(dsc.x));
+        const gptr<int32_t> COL = as_global(dsc.col);
+        const gptr<int64_t> RP = as_global(dsc.row_ptr);
+        const gptr<double> Y = as_global(dsc.y);
+        const gptr<double> STEPS = as_global(L.steps);
+        const gptr<int32_t> RIDX = dsc.rows ? as_global(dsc.rows) : nullptr;
+        unsigned done = 0;
+        const gptr<int32_t> dummy_i = as_global((const int32_t*)(V + d + lane));   // valid, unused
+        const gptr<S> dummy_s = as_global((const S*)(V + d + 2 * lane));
+        struct Batch { int64_t rb, re; double y, s; };
+        auto load_batch = [&](int64_t g) __attribute__((always_inline)) -> Batch {
+            Batch bt{0, 0, 0.0, 0.0};
+            const int64_t ti = g + lane;
+            if (ti < n) {
+                const int64_t r = RIDX ? (int64_t)RIDX[ti] : ti;
+                bt.rb = RP[r];
+                bt.re = RP[r + 1];
+                bt.y = Y[ti];
+                bt.s = STEPS[ti];
+            }
+            return bt;
+        };
+        struct Group { int32_t ca[8], cb[8]; S xa[8], xb[8]; bool ia[8], ic[8]; };
+        auto rl64 = [&](int64_t v, int i) __attribute__((always_inline)) -> int64_t {
+            return (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v & 0xffffffff), i) |
+                   ((int64_t)__builtin_amdgcn_readlane((int)(v >> 32), i) << 32);
+        };
+        // entries of rows g + i0 .. g + i0 + 7 of batch bt: unconditional loads (masked-off
+        // entries read valid dummy addresses), so the compiler counts them without branches
+        auto load_group = [&](const Batch& bt, int i0, Group& G) __attribute__((always_inline)) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int64_t b = rl64(bt.rb, i0 + q), e = rl64(bt.re, i0 + q);
+                const int64_t ka = b + lane, kc = b + 64 + lane;
+                const bool ia = ka < e, ic = kc < e;
+                G.ca[q] = *(ia ? &COL[ka] : dummy_i);
+                const S xa = *(ia ? &X[ka] : dummy_s);
+                G.cb[q] = *(ic ? &COL[kc] : dummy_i);
+                const S xb = *(ic ? &X[kc] : dummy_s);
+                G.xa[q] = ia ? xa : S(0);
+                G.xb[q] = ic ? xb : S(0);
+                G.ia[q] = ia;
+                G.ic[q] = ic;
+            }
+        };
+        // rows u0 .. u0 + 7 (those < n_fill) into their slots, each once the chain is done with the
+        // row its slot held (row u - SR, read by the chain up to row u - SR + SK), published row
+        // by row: the chain at sample t waits for row t + SK + 1
+        auto stage_group = [&](int64_t u0, const Group& G) __attribute__((always_inline)) -> bool {
+            bool good = true;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int64_t u = u0 + q;
+                if (good && u < n_fill) {
+                    good = wait_for(done, &hdr->done, u - SR + SK + 1, 16);
+                    LdsSlot& sl = slots[u & (SR - 1)];
+                    sl.col[lane] = G.ca[q];
+                    sl.col[lane + 64] = G.cb[q];
+                    sl.val[lane] = float(G.xa[q]);
+                    sl.val[lane + 64] = float(G.xb[q]);
+                    if constexpr (!TAIL) {
+                        // every feature in LDS: the entry's read and write address is W[j]
+                        // (no tagger); inactive entries have x = 0 and use the dummy dword
+                        const unsigned ha = G.ia[q] ? kWoff + (unsigned)G.ca[q] : kLdsDummy;
+                        const unsigned hb = G.ic[q] ? kWoff + (unsigned)G.cb[q] : kLdsDummy;
+                        sl.rw[lane] = ha | (ha << 16);
+                        sl.rw[lane + 64] = hb | (hb << 16);
+                        publish(&hdr->tagged, u + 1);
+                    }
+                    publish(&hdr->loaded, u + 1);
+                }
+            }
+            return good;
+        };
+        Batch cur = load_batch(0);
+        Group GA, GB;
+        load_group(cur, 0, GA);
+        for (int64_t g = 0; g < n_fill; g += 64) {
+            const Batch nxt = load_batch(g + 64);
+            // meta of rows g .. g + 63: their ring positions held rows g - 128 .. g - 65
+            if (!wait_for(done, &hdr->done, g - 64, 16)) break;
+            {
+                const int m = (int)((g + lane) & (kMetaRing - 1));
+                meta->y[m] = float(cur.y);
+                meta->s[m] = float(cur.s);
+                meta->s64[m] = cur.s;
+                meta->nnz[m] = (int32_t)(cur.re - cur.rb);
+            }
+            bool ok = true;
+            static_for<4>([&](auto kc) {
+                // group i0 is in GA; fetch group i0 + 8 into GB, stage GA; then the other way
+                constexpr int i0 = 16 * decltype(kc)::value;
+                if (!ok) return;
+                load_group(cur, i0 + 8, GB);
+                ok = stage_group(g + i0, GA);
+                if constexpr (i0 + 16 < 64) load_group(cur, i0 + 16, GA);
+                else load_group(nxt, 0, GA);
+                if (ok) ok = stage_group(g + i0 + 8, GB);
+            });
+            if (!ok) break;
+            cur = nxt;
+        }
+        stamp_out(1);
+        return;
+    }
+
+    if (wave == 2 && !TAIL) return;   // the loader writes the addresses
+    if (wave == 2) {
+        // ---------------- tagger: tail tags and each entry's LDS read / write address ----------
+        // Four rows per step, so that their LDS round trips overlap: the rows' columns, then the
+        // sweeps, then each row's tag lookups and updates in row order (one wave's LDS operations
+        // execute in program order, so row u+1's lookups see row u's updates), then the rows'
+        // addresses.
+        constexpr int TB = 4;
+        unsigned loaded = 0;
+        uint16_t* dtag = reinterpret_cast<uint16_t*>(&hdr->dtag);
+        const int64_t chunk = ((T + kSweepRows - 1) / kSweepRows + 255) & ~int64_t(255);
+        static_assert(8 % TB == 0, "n_fill is a multiple of TB");
+        for (int64_t u0 = 0; u0 < n_fill; u0 += TB) {
+            constexpr int nb = TB;
+            if (!wait_for(loaded, &hdr->loaded, u0 + nb, 32)) break;
+            int nnz[TB];
+            int32_t ca[TB], cb[TB];
+#pragma unroll
+            for (int q = 0; q < TB; ++q) {
+                const int64_t u = u0 + q;
+                const LdsSlot& sl = slots[u & (SR - 1)];
+                nnz[q] = meta->nnz[u & (kMetaRing - 1)];
+                ca[q] = sl.col[lane];
+                cb[q] = sl.col[lane + 64];
+            }
+            // sweep the chunks of rows u0 .. u0 + TB - 1, keeping the tags of rows u0 - SK .. u0 - 1
+            // (the oldest rows this step's lookups need); each chunk is swept at least every
+            // kSweepRows rows, so no tag outlives 256 rows
+#pragma unroll
+            for (int q = 0; q < TB; ++q) {
+                const int64_t lo = ((u0 + q) & (kSweepRows - 1)) * chunk;
+                const int64_t hi = lo + chunk < T ? lo + chunk : T;
+                for (int64_t i = lo + 4 * lane; i < hi; i += 256) {
+                    const uint64_t v = *reinterpret_cast<const uint64_t*>(tagpos + i);
+                    uint64_t o = 0;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const unsigned tg = (unsigned)(v >> (16 * k)) & 0xFFFF;
+                        const unsigned dl = ((unsigned)u0 - (tg >> 8)) & 255;
+                        const bool live = tg != 0xFFFF && dl >= 1 && dl <= SK;
+                        o |= (uint64_t)(live ? tg : 0xFFFFu) << (16 * k);
+                    }
+                    *reinterpret_cast<uint64_t*>(tagpos + i) = o;
+                }
+            }
+            unsigned va[TB], vb[TB];
+#pragma unroll
+            for (int q = 0; q < TB; ++q) {
+                const int64_t u = u0 + q;
+                const bool ta_on = lane < nnz[q] && ca[q] >= K, tb_on = lane + 64 < nnz[q] && cb[q] >= K;
+                uint16_t* pa = ta_on ? tagpos + (ca[q] - K) : dtag;
+                uint16_t* pb = tb_on ? tagpos + (cb[q] - K) : dtag;
+                va[q] = *pa;
+                vb[q] = *pb;
+                const unsigned tag = (unsigned)(u & 255) << 8;
+                *pa = (uint16_t)(tag | (unsigned)lane);
+                *pb = (uint16_t)(tag | (unsigned)(lane + 64));
+            }
+#pragma unroll
+            for (int q = 0; q < TB; ++q) {
+                const int64_t u = u0 + q;
+                auto rw_of = [&](int e, int32_t c, unsigned v) __attribute__((always_inline)) -> uint32_t {
+                    const bool tail = c >= K;
+                    const unsigned dl = ((unsigned)u - (v >> 8)) & 255;
+                    const bool prev = v != 0xFFFF && dl >= 1 && dl <= SK;
+                    const unsigned rd_tail = prev ? val_off(u - dl) + (v & 255) : kLdsDummy;
+                    const unsigned wr_tail = val_off(u) + (unsigned)e;
+                    const unsigned head = kWoff + (unsigned)c;
+                    const unsigned rd = e >= nnz[q] ? kLdsDummy : tail ? rd_tail : head;
+                    const unsigned wr = e >= nnz[q] ? kLdsDummy : tail ? wr_tail : head;
+                    return rd | (wr << 16);
+                };
+                if (q < nb) {
+                    LdsSlot& sl = slots[u & (SR - 1)];
+                    sl.rw[lane] = rw_of(lane, ca[q], va[q]);
+                    sl.rw[lane + 64] = rw_of(lane + 64, cb[q], vb[q]);
+                }
+            }
+            publish(&hdr->tagged, u0 + nb);
+        }
+        stamp_out(2);
+        return;
+    }
+
+    // ---------------- chain ----------------
+    // The per-sample code is straight-line: the flag checks come before the LDS reads they
+    // guard and branch only to a spin, so no read result crosses a branch (a join would make
+    // the compiler wait for it). The loop runs a multiple of SK + 1 samples; samples past n are
+    // null (no entries, LDS traffic to the dummy dword, no loss), so every gather's registers
+    // have a consumer: the compiler treats an asm load's result as written at issue, and a dead
+    // one's registers could be reused while the load is still in flight.
+    double alpha = 1.0;       // SquaredL2: w = alpha * v
+    double loss_sum = 0.0;
+    float loss_blk = 0.0f;
+    int64_t count = 0;
+    unsigned loaded = 0, tagged = 0;
+    // Target of masked-off gather / store lanes: 16 rotating 256-byte rows, a different one for
+    // each of the 4 VMEM instructions of 4 consecutive samples (accesses to one line from one
+    // wave are processed in order in L2; one shared dummy line serialised the chain's stream).
+    auto dummy = [&](int64_t t, int k) __attribute__((always_inline)) -> float* {
+        return V + d + 128 + (int)(((4 * t + k) & 15) << 6) + lane;
+    };
+    // gathered tail weights: row u's in gr[u % (SK + 1)]. A gather's registers are written by
+    // the load when it lands, so they are never copied before their s_waitcnt: the gather of
+    // row t + SK goes to the set row t - 1 used, and the loop is unrolled SK + 1 times
+    float gr[GS][2];
+    bool ok = true;
+    // wait until rows < nl are loaded and rows < nt tagged (the spin path only)
+    auto need = [&](int64_t nl, int64_t nt) __attribute__((always_inline)) {
+        nl = nl < n_fill ? nl : n_fill;
+        nt = nt < n_fill ? nt : n_fill;
+        if ((int64_t)loaded < nl || (int64_t)tagged < nt) {
+            ok = ok && wait_for(loaded, &hdr->loaded, nl, 2);
+            ok = ok && wait_for(tagged, &hdr->tagged, nt, 4);
+        }
+    };
+    // the entries of row u a gather needs
+    struct GCols { int32_t c0, c1; int nnz; };
+    auto gcols = [&](int64_t u) __attribute__((always_inline)) -> GCols {
+        const LdsSlot& sl = slots[u & (SR - 1)];
+        const int nz = meta->nnz[u & (kMetaRing - 1)];
+        return GCols{sl.col[lane], sl.col[lane + 64], nz};
+    };
+    // Only tail entries touch memory: the other lanes are masked off (lane 63 always runs, on a
+    // dummy address when it has no tail entry, so no instruction has an empty EXEC and each
+    // still counts once in vmcnt); a scattered VMEM instruction costs its issue per address.
+    auto gather = [&](const GCols& G, float (&g)[2], int64_t t) __attribute__((always_inline)) {
+        const bool a0 = lane < G.nnz && G.c0 >= K, a1 = lane + 64 < G.nnz && G.c1 >= K;
+        g[0] = gather_sc1_masked(a0 ? V + G.c0 : dummy(t, 0), ballot_or63(a0));
+        g[1] = gather_sc1_masked(a1 ? V + G.c1 : dummy(t, 1), ballot_or63(a1));
+    };
+    // the data of sample t
+    struct Row { float x0, x1; uint32_t rw0, rw1; int32_t c0, c1; int nnz; float y, s; double s64; };
+    auto row_of = [&](int64_t t) __attribute__((always_inline)) -> Row {
+        const LdsSlot& sl = slots[t & (SR - 1)];
+        const int m = (int)(t & (kMetaRing - 1));
+        return Row{sl.val[lane], sl.val[lane + 64], sl.rw[lane], sl.rw[lane + 64], sl.col[lane],
+                   sl.col[lane + 64], meta->nnz[m], meta->y[m], meta->s[m], L2 ? meta->s64[m] : 0.0};
+    };
+    // prologue: gathers of rows 0 .. SK-1, each followed by two (dummy) stores, the same VMEM
+    // pattern as a sample of the loop; then the columns of row SK and the data of sample 0
+    GCols gc{0, 0, 0};
+    if constexpr (TAIL) {
+        static_for<SK>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            need(q + 1, 0);
+            gather(gcols(q), gr[q], q);
+            store_f32(dummy(q, 2), 0.0f);
+            store_f32(dummy(q, 3), 0.0f);
+        });
+        need(SK + 1, 1);
+        gc = gcols(SK);
+    } else {
+        need(0, 1);
+    }
+    Row cur = row_of(0);
+    auto sample = [&](auto qc, int64_t t) __attribute__((always_inline)) {
+        constexpr int Q = decltype(qc)::value;           // t % GS
+        constexpr int QN = (Q + SK) % GS;                 // (t + SK) % GS
+        // the rows the reads below need (a branch to the spin only)
+        need(TAIL ? t + SK + 2 : 0, t + 2);
+        // this sample's weight reads (after the previous sample's writes, in program order),
+        // row t + SK's gather, then the columns of row t + SK + 1 and the data of sample t + 1:
+        // all issued before anything waits (the scheduling barrier keeps the compiler from
+        // sinking the prefetch below the arithmetic), so their LDS round trips overlap
+        const unsigned r0 = cur.rw0 & 0xFFFF, r1 = cur.rw1 & 0xFFFF;
+        const float l0 = lds[r0], l1 = lds[r1];
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (TAIL) {
+            gather(gc, gr[QN], t);
+            gc = gcols(t + SK + 1);
+        }
+        const Row nxt = row_of(t + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        float w0 = l0, w1 = l1;
+        if constexpr (TAIL) {
+            // row t's gather: issued SK samples ago, followed by 4 SK VMEM instructions
+            // (PSGD_STAMPS: the time this wait takes is the chain's "wait" counter)
+            uint64_t vm0 = 0;
+            if (L.stamps) vm0 = __builtin_amdgcn_s_memtime();
+            asm volatile("s_waitcnt vmcnt(%2)" : "+v"(gr[Q][0]), "+v"(gr[Q][1]) : "i"(4 * SK) : "memory");
+            if (L.stamps) st_wait += __builtin_amdgcn_s_memtime() - vm0;
+            // head: W[j]; tail also in rows t-SK .. t-1: that row's new value; else the gather
+            w0 = r0 == kLdsDummy ? gr[Q][0] : l0;
+            w1 = r1 == kLdsDummy ? gr[Q][1] : l1;
+        }
+        w0 = lane < cur.nnz ? w0 : 0.0f;
+        w1 = lane + 64 < cur.nnz ? w1 : 0.0f;
+        float acc = cur.x0 * w0;
+        acc = __builtin_fmaf(cur.x1, w1, acc);
+        float z = wave_sum_uniform(acc);
+        if constexpr (L2) {
+            z = float(alpha * double(z));
+            alpha *= 1.0 - cur.s64 * kp.reg;
+        }
+        float loss;
+        const float c = sparse_coef<GRAD>(z, cur.y, cur.s, loss);
+        loss_blk += t < n ? loss : 0.0f;
+        if ((t & 31) == 31) { loss_sum += double(loss_blk); loss_blk = 0.0f; }
+        const float cv = L2 ? float(double(c) / alpha) : c;
+        const float nv0 = __builtin_fmaf(cv, cur.x0, w0);
+        const float nv1 = __builtin_fmaf(cv, cur.x1, w1);
+        lds[cur.rw0 >> 16] = nv0;
+        lds[cur.rw1 >> 16] = nv1;
+        // this row's tail stores (2 VMEM instructions)
+        if constexpr (TAIL) {
+            const bool a0 = lane < cur.nnz && cur.c0 >= K, a1 = lane + 64 < cur.nnz && cur.c1 >= K;
+            store_f32_masked(a0 ? V + cur.c0 : dummy(t, 2), nv0, ballot_or63(a0));
+            store_f32_masked(a1 ? V + cur.c1 : dummy(t, 3), nv1, ballot_or63(a1));
+        }
+        publish(&hdr->done, t + 1);
+        cur = nxt;
+    };
+    for (int64_t t = 0; ok && t < n_pad; t += GS)
+        static_for<GS>([&](auto qc) { sample(qc, t + decltype(qc)::value); });
+    count = ok ? n : 0;
+    __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // the last gathers' registers stay allocated until they have landed
+#pragma unroll
+    for (int q = 0; q < GS; ++q) asm volatile("" : : "v"(gr[q][0]), "v"(gr[q][1]));
+    stamp_out(0);
+    loss_sum += double(loss_blk);
+    if constexpr (GRAD == G_LEAST_SQUARES) loss_sum = loss_sum / 2.0;
+    // the chain's weights (w = alpha v) and regVal of its last update (PSGD.scala:257)
+    double nsq = 0.0;
+    double* wo = L.w_out + (int64_t)chain * d;
+    for (int i = lane; i < d; i += 64) {
+        const float v = i < K ? W[i] : __hip_atomic_load(&V[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const double wv = alpha * double(v);
+        wo[i] = wv;
+        if constexpr (L2) nsq += wv * wv;
+    }
+    double rv = 0.0;
+    if constexpr (L2) {
+        nsq = wave_sum(nsq);
+        if (count > 0) {
+            const double nrm = sqrt(nsq);
+            rv = 0.5 * kp.reg * nrm * nrm;
+        }
+    }
+    if (lane == 0) {
+        L.rv[chain] = rv;
+        L.loss[chain] = loss_sum;
+        L.cnt[chain] = count;
+        L.cnt_d[chain] = double(count);
+    }
+}
+
+template <typename S, int GRAD, int SK>
+static int lds_upd(const ChainLaunch& L, const KParams& kp, int upd, int K, size_t lds, hipStream_t st) {
+    auto k = K < kp.d ? (upd == U_SIMPLE ? chain_sparse_lds<S, GRAD, U_SIMPLE, SK, true>
+                                         : chain_sparse_lds<S, GRAD, U_SQUARED_L2, SK, true>)
+                      : (upd == U_SIMPLE ? chain_sparse_lds<S, GRAD, U_SIMPLE, SK, false>
+                                         : chain_sparse_lds<S, GRAD, U_SQUARED_L2, SK, false>);
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(192), lds, st, L, kp, K);
+    return (int)hipGetLastError();
+}
+
+template <typename S, int SK>
+static int lds_grad(const ChainLaunch& L, const KParams& kp, int grad, int upd, int K, size_t lds, hipStream_t st) {
+    switch (grad) {
+    case G_LOGISTIC: return lds_upd<S, G_LOGISTIC, SK>(L, kp, upd, K, lds, st);
+    case G_LEAST_SQUARES: return lds_upd<S, G_LEAST_SQUARES, SK>(L, kp, upd, K, lds, st);
+    case G_HINGE: return lds_upd<S, G_HINGE, SK>(L, kp, upd, K, lds, st);
+    default: return -3;
+    }
+}
+
+template <int SK>
+static int lds_launch(const ChainLaunch& L, const KParams& kp, int storage, int gradient, int updater,
+                      hipStream_t stream, int* kernel_variant) {
+    int64_t K = lds_head<SK>(kp.d);
+    if (K < 0) return -3;
+    // tests: PSGD_SPARSE_LDS_HEAD=k caps the LDS-resident head (exercises the tail at small d)
+    if (const char* e = getenv("PSGD_SPARSE_LDS_HEAD"))
+        if (*e) { const int64_t cap = atoll(e) & ~int64_t(3); if (cap >= 0 && cap < K) K = cap; }
+    const size_t lds = (size_t)lds_bytes<SK>(kp.d, K);
+    if (kernel_variant) *kernel_variant = 600 + (SK == 8 ? 10 : 0) + storage;
+    if (storage == 1) return lds_grad<float, SK>(L, kp, gradient, updater, (int)K, lds, stream);
+    return lds_grad<double, SK>(L, kp, gradient, updater, (int)K, lds, stream);
+}
+
+// Speculation depth: 4 rows by default (tail gathers are L2 hits once the tails fit L2);
+// PSGD_SPARSE_SK=8 for A/B measurements (read at every launch).
+static int lds_depth() {
+    const char* e = getenv("PSGD_SPARSE_SK");
+    return (e && atoi(e) == 8) ? 8 : 4;
+}
+
+bool sparse_lds_applies(int64_t d, int64_t max_nnz) {
+    if (max_nnz > LCAP) return false;
+    return (lds_depth() == 8 ? lds_head<8>(d) : lds_head<4>(d)) >= 0;
+}
+
+int64_t sparse_lds_head(int64_t d) { return lds_depth() == 8 ? lds_head<8>(d) : lds_head<4>(d); }
+
+int launch_sparse_lds_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
+                             int updater, int64_t max_nnz, hipStream_t stream, int* kernel_variant) {
+    if (kp.n_chains <= 0) return 0;
+    if (!sparse_lds_applies(kp.d, max_nnz)) return -3;
+    if (!L.wf32 || L.wstride < (int64_t)kp.d + 128 + 1024) return (int)hipErrorInvalidValue;
+    if (lds_depth() == 8) return lds_launch<8>(L, kp, storage, gradient, updater, stream, kernel_variant);
+    return lds_launch<4>(L, kp, storage, gradient, updater, stream, kernel_variant);
+}
+
+}  // namespace psgd

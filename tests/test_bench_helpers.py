@@ -19,6 +19,7 @@ def test_pmc_traffic_none_for_unprofiled_kernels():
 def test_kernel_labels():
     assert bench.kernel_name(302).startswith("chain_block (NV=2")
     assert bench.kernel_name(411).startswith("chain_sparse_spec")
+    assert bench.kernel_name(601).startswith("chain_sparse_lds")
     assert bench.kernel_name(401).startswith("chain_sparse (")
     assert bench.kernel_name(101).startswith("chain_dense")
 

@@ -3,7 +3,8 @@
 * C1 (Logistic dense 100k x 100 fp64, 4 partitions, 10 iterations) at full size, tol 0 and
   tol 0.001 (the per-sample break): exact chain counts, 1e-9 weights/loss.
 * C4 (Hinge CSR, rcv1-like: d = 47,236, 60-128 nnz/row, rows L2-normalised) on 256 chains:
-  fp32 through chain_sparse_spec (variant 411, its 94 KB LDS tag table at this d) and fp64
+  fp32 through chain_sparse_lds (variant 601: an LDS head of ~22k features, the tail in HBM) and
+  chain_sparse_spec (variant 411, its 94 KB LDS tag table at this d), and fp64
   through chain_general (variant 201).
 * C5 (L2 Logistic CSR, d = 2^22, 100 nnz/row, lambda 1e-6, step 0.5): fp32 chain_sparse
   (variant 401, HBM-resident weights) and fp64 chain_general's alpha-scaled lazy SquaredL2.
@@ -123,13 +124,16 @@ def c4():
     return d, rp, col, val, y, offs
 
 
-def test_c4_rcv1_shape_fp32(pkg, oracle, c4):
+@pytest.mark.parametrize("kernel,variant", [("lds", 601), ("spec", 411)])
+def test_c4_rcv1_shape_fp32(pkg, oracle, c4, kernel, variant, monkeypatch):
+    # chain_sparse_lds (LDS head of ~22k features, tail in HBM) and chain_sparse_spec (94 KB tag table)
+    monkeypatch.setenv("PSGD_SPARSE_KERNEL", kernel)
     d, rp, col, val, y, offs = c4
     v32 = val.astype(np.float32)
     data = csr_parts(pkg, y, rp, col, v32, d, offs)
     w, h, counts = pkg.runParallelizedSGD(data, pkg.HingeGradient(), pkg.SimpleSGDUpdater(), 1.0, 3, 0.0, 1.0,
                                           np.zeros(d), 0.0, compute_dtype="f32", return_chain_counts=True)
-    assert pkg.optimization.get_context(0).last_kernel() == 411   # chain_sparse_spec, f32 rows
+    assert pkg.optimization.get_context(0).last_kernel() == variant
     mat = oracle.Matrix(y, row_ptr=rp, col=col, val=v32.astype(np.float64), d=d)
     wr, hr, cr = oracle.run(mat, offs, "hinge", "simple", 1.0, 3, 0.0, np.zeros(d), tol=0.0, n_threads=8)
     assert [list(map(int, c)) for c in counts] == [list(map(int, c)) for c in cr]

@@ -1,4 +1,9 @@
-"""The fp32 CSR chain kernel (psgd_sparse.hip) against the fp64 CPU oracle.
+"""The fp32 CSR chain kernels (psgd_sparse_lds.hip, psgd_sparse.hip) against the fp64 CPU oracle.
+
+Every case runs on each kernel variant (PSGD_SPARSE_KERNEL forces one): chain_sparse_lds with
+all weights in LDS, with an LDS head of d/3 features and the rest in HBM (PSGD_SPARSE_LDS_HEAD:
+exercises the tail gathers and their corrections at small d) at speculation depths 4 and 8,
+chain_sparse_spec, and chain_sparse.
 
 fp32 compute is the throughput mode; its stated tolerance is weights within
 FP32_REL * max|w| and the loss history within FP32_LOSS_REL relative of the fp64 oracle on the
@@ -29,6 +34,28 @@ def need_gpu():
         pytest.skip("no GPU")
 
 
+KERNELS = {  # name: (environment, variant base without the storage digit)
+    "lds": ({"PSGD_SPARSE_KERNEL": "lds"}, 600),
+    "lds_tail": ({"PSGD_SPARSE_KERNEL": "lds", "PSGD_SPARSE_LDS_HEAD": "third"}, 600),
+    "lds_tail_sk8": ({"PSGD_SPARSE_KERNEL": "lds", "PSGD_SPARSE_LDS_HEAD": "third", "PSGD_SPARSE_SK": "8"}, 610),
+    "spec": ({"PSGD_SPARSE_KERNEL": "spec"}, 410),
+    "plain": ({"PSGD_SPARSE_KERNEL": "plain"}, 400),
+}
+
+
+@pytest.fixture(params=sorted(KERNELS))
+def kernel(request, monkeypatch):
+    env, base = KERNELS[request.param]
+    for k in ("PSGD_SPARSE_KERNEL", "PSGD_SPARSE_LDS_HEAD", "PSGD_SPARSE_SK"):
+        monkeypatch.delenv(k, raising=False)
+
+    def apply(d):
+        for k, v in env.items():
+            monkeypatch.setenv(k, str(max(d // 3, 0)) if v == "third" else v)
+        return base
+    return apply
+
+
 def synth_csr(rng, n, d, kmin, kmax, grad):
     rp, col, val = [0], [], []
     for _ in range(n):
@@ -49,7 +76,9 @@ def synth_csr(rng, n, d, kmin, kmax, grad):
     return rp, col, val, y
 
 
-def check(pkg, oracle, rp, col, val, y, d, offs, grad, upd, step, reg, iters, frac=1.0, dtype=np.float32):
+def check(pkg, oracle, rp, col, val, y, d, offs, grad, upd, step, reg, iters, frac=1.0, dtype=np.float32,
+          kernel=None):
+    base = kernel(d) if kernel else None
     vstore = val.astype(dtype)
     parts = [pkg.CsrPartition(y[a:b], rp[a:b + 1] - rp[a], col[rp[a]:rp[b]], vstore[rp[a]:rp[b]], d)
              for a, b in zip(offs[:-1], offs[1:])]
@@ -57,9 +86,12 @@ def check(pkg, oracle, rp, col, val, y, d, offs, grad, upd, step, reg, iters, fr
     w, h, counts = pkg.runParallelizedSGD(data, getattr(pkg, G[grad])(), getattr(pkg, U[upd])(), step,
                                           iters, reg, frac, np.zeros(d), 0.0, compute_dtype="f32",
                                           return_chain_counts=True)
-    # 41x: gathers SK samples ahead (rows <= 128 non-zeros, tag table in LDS); 40x: one per sample
-    spec = int(np.max(np.diff(rp))) <= 128
-    want = (410 if spec else 400) + (1 if dtype == np.float32 else 0)
+    # 60x/61x: weights in LDS; 41x: gathers SK samples ahead (tag table in LDS); 40x: one per
+    # sample. Rows of more than 128 non-zeros always take 40x.
+    wide = int(np.max(np.diff(rp))) > 128
+    if base is None:
+        base = 600
+    want = (400 if wide else base) + (1 if dtype == np.float32 else 0)
     assert pkg.optimization.get_context(0).last_kernel() == want
     mat = oracle.Matrix(y, row_ptr=rp, col=col, val=vstore.astype(np.float64), d=d)
     wr, hr, cr = oracle.run(mat, offs, grad, upd, step, iters, reg, np.zeros(d), tol=0.0, fraction=frac,
@@ -75,23 +107,23 @@ def check(pkg, oracle, rp, col, val, y, d, offs, grad, upd, step, reg, iters, fr
 
 @pytest.mark.parametrize("grad", ["least_squares", "logistic", "hinge"])
 @pytest.mark.parametrize("upd", ["simple", "squared_l2"])
-def test_sparse_wide(pkg, oracle, grad, upd):
+def test_sparse_wide(pkg, oracle, grad, upd, kernel):
     rng = np.random.default_rng(len(grad) * 7 + len(upd))
     n, d = 1500, 3000
     rp, col, val, y = synth_csr(rng, n, d, 0, 40, grad)
     offs = [0, 500, 500, 501, 1500]
-    check(pkg, oracle, rp, col, val, y, d, offs, grad, upd, 0.3, 0.05, 3)
+    check(pkg, oracle, rp, col, val, y, d, offs, grad, upd, 0.3, 0.05, 3, kernel=kernel)
 
 
 @pytest.mark.parametrize("grad", ["least_squares", "logistic", "hinge"])
-def test_sparse_narrow_overlapping_rows(pkg, oracle, grad):
+def test_sparse_narrow_overlapping_rows(pkg, oracle, grad, kernel):
     # d = 12 with up to 9 non-zeros per row: nearly every feature is shared by consecutive rows
     rng = np.random.default_rng(3 + len(grad))
     n, d = 900, 12
     rp, col, val, y = synth_csr(rng, n, d, 1, 9, grad)
     offs = [0, 300, 600, 900]
-    check(pkg, oracle, rp, col, val, y, d, offs, grad, "simple", 0.2, 0.0, 3)
-    check(pkg, oracle, rp, col, val, y, d, offs, grad, "squared_l2", 0.2, 0.1, 2)
+    check(pkg, oracle, rp, col, val, y, d, offs, grad, "simple", 0.2, 0.0, 3, kernel=kernel)
+    check(pkg, oracle, rp, col, val, y, d, offs, grad, "squared_l2", 0.2, 0.1, 2, kernel=kernel)
 
 
 def test_sparse_rows_wider_than_128(pkg, oracle):
@@ -102,20 +134,21 @@ def test_sparse_rows_wider_than_128(pkg, oracle):
     check(pkg, oracle, rp, col, val, y, d, [0, 200, 400], "hinge", "squared_l2", 0.5, 0.02, 2)
 
 
-def test_sparse_sampled_batches(pkg, oracle):
+def test_sparse_sampled_batches(pkg, oracle, kernel):
     rng = np.random.default_rng(12)
     n, d = 2000, 500
     rp, col, val, y = synth_csr(rng, n, d, 0, 30, "hinge")
     for frac in (0.15, 0.6):
-        check(pkg, oracle, rp, col, val, y, d, [0, 1000, 2000], "hinge", "simple", 0.5, 0.0, 3, frac=frac)
+        check(pkg, oracle, rp, col, val, y, d, [0, 1000, 2000], "hinge", "simple", 0.5, 0.0, 3, frac=frac,
+              kernel=kernel)
 
 
-def test_sparse_f64_storage(pkg, oracle):
+def test_sparse_f64_storage(pkg, oracle, kernel):
     rng = np.random.default_rng(13)
     n, d = 800, 200
     rp, col, val, y = synth_csr(rng, n, d, 0, 20, "logistic")
     check(pkg, oracle, rp, col, val, y, d, [0, 400, 800], "logistic", "simple", 0.5, 0.0, 2,
-          dtype=np.float64)
+          dtype=np.float64, kernel=kernel)
 
 
 def test_sparse_device_registration(pkg, oracle):
