@@ -90,9 +90,14 @@ int32_t psgd_ctx_destroy(psgd_ctx* ctx);
  * is copied to HBM once (the analogue of RDD.cache(), ParallelizedSGDSuite.scala:88) and no host
  * pointer is kept. Rows are in the partition's iterator order. labels[n_rows] are doubles;
  * x is row-major n_rows x d of `dtype`. Thread-safe (Spark local[N] registers from N task
- * threads). Empty partitions (n_rows == 0) must be registered too: they take part in the
- * combine with count 0 (PSGD.scala:270-276). Replaces the mapPartitions closure input at
- * PSGD.scala:243-253. */
+ * threads; their copies run concurrently). Empty partitions (n_rows == 0) must be registered
+ * too: they take part in the combine with count 0 (PSGD.scala:270-276). Replaces the
+ * mapPartitions closure input at PSGD.scala:243-253.
+ * Ingest: pinned sources (psgd_host_alloc) are DMA'd directly and waited for; pageable ones are
+ * packed through the context's pinned staging ring, the DMA of one chunk overlapping the packing
+ * of the next, on a copy stream of their own. The call returns once the caller's memory has been
+ * read (the last chunks may still be in flight from the library's buffers); the next epoch waits
+ * for them on the device, psgd_register_wait on the host. */
 int32_t psgd_register_dense(psgd_ctx* ctx, int64_t part, int64_t n_rows, int32_t d,
                             const double* labels, const void* x, int32_t dtype);
 
@@ -116,6 +121,14 @@ int32_t psgd_register_dense_device(psgd_ctx* ctx, int64_t part, int64_t n_rows, 
 int32_t psgd_register_csr_device(psgd_ctx* ctx, int64_t part, int64_t n_rows, int32_t d,
                                  const double* d_labels, const int64_t* d_row_ptr,
                                  const int32_t* d_col, const void* d_val, int32_t dtype);
+
+/* Page-locked host buffers for packing partitions in place (the JVM shim wraps them as direct
+ * ByteBuffers, NewDirectByteBuffer): registration from them skips the staging copy. */
+int32_t psgd_host_alloc(psgd_ctx* ctx, int64_t bytes, void** out);
+int32_t psgd_host_free(psgd_ctx* ctx, void* p);
+
+/* Block until every registration copy enqueued so far has landed in HBM. */
+int32_t psgd_register_wait(psgd_ctx* ctx);
 
 int32_t psgd_clear_partitions(psgd_ctx* ctx);
 int32_t psgd_num_partitions(psgd_ctx* ctx, int64_t* n_parts, int64_t* n_rows_total);

@@ -24,7 +24,7 @@ EXPORTED = (
     "psgd_clear_partitions", "psgd_num_partitions", "psgd_run_epoch", "psgd_run_epoch_device",
     "psgd_fold_partials_device", "psgd_convergence_terms_device", "psgd_initial_regval",
     "psgd_ctx_last_kernel", "psgd_ctx_last_chain_ms", "psgd_libsvm_read", "psgd_libsvm_free",
-    "psgd_sample_partition",
+    "psgd_sample_partition", "psgd_host_alloc", "psgd_host_free", "psgd_register_wait",
 )
 
 
@@ -105,6 +105,9 @@ def lib():
             "psgd_libsvm_read": ([C.c_char_p, C.c_int32, C.c_int32, C.POINTER(C.POINTER(psgd_libsvm))], C.c_int32),
             "psgd_libsvm_free": ([C.POINTER(psgd_libsvm)], None),
             "psgd_sample_partition": ([C.c_int32, C.c_int64, C.c_int64, C.c_double, vp, i64p], C.c_int32),
+            "psgd_host_alloc": ([vp, C.c_int64, C.POINTER(vp)], C.c_int32),
+            "psgd_host_free": ([vp, vp], C.c_int32),
+            "psgd_register_wait": ([vp], C.c_int32),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -134,6 +137,24 @@ def sample_partition(seed: int, n: int, fraction: float, device: int = 0):
     check(lib().psgd_sample_partition(device, int(seed), int(n), float(fraction), rows.ctypes.data,
                                       C.byref(m)))
     return rows[: m.value].copy()
+
+
+class _PinnedBuffer:
+    """Page-locked host memory from psgd_host_alloc; freed when the last numpy view of it goes
+    (the context must outlive it)."""
+
+    def __init__(self, ctx, addr, nbytes):
+        self._ctx, self._addr = ctx, addr
+        self.view = (C.c_char * nbytes).from_address(addr)
+        self.view.owner = self      # numpy views keep the ctypes array, which keeps this
+
+    def __del__(self):
+        try:
+            if self._ctx.handle and self._addr:
+                self._ctx._L.psgd_host_free(self._ctx.handle, self._addr)
+        except Exception:
+            pass
+        self._addr = None
 
 
 class Context:
@@ -188,6 +209,21 @@ class Context:
     def register_csr_device(self, part, n_rows, d, labels_ptr, row_ptr_ptr, col_ptr, val_ptr, dtype):
         check(self._L.psgd_register_csr_device(self.handle, part, n_rows, d, labels_ptr, row_ptr_ptr,
                                                col_ptr, val_ptr, dtype))
+
+    def register_wait(self):
+        """Block until every registration copy has landed in HBM (psgd_register_wait)."""
+        check(self._L.psgd_register_wait(self.handle))
+
+    def host_array(self, shape, dtype):
+        """A numpy array over page-locked host memory (psgd_host_alloc): registration from it is
+        one direct DMA, no staging copy. Freed with the returned array's owner (`.base`)."""
+        import numpy as np
+        dt = np.dtype(dtype)
+        n = int(np.prod(shape)) * dt.itemsize
+        p = C.c_void_p()
+        check(self._L.psgd_host_alloc(self.handle, max(n, 1), C.byref(p)))
+        buf = _PinnedBuffer(self, p.value, max(n, 1))
+        return np.frombuffer(buf.view, dtype=dt, count=int(np.prod(shape))).reshape(shape)
 
     def clear(self):
         check(self._L.psgd_clear_partitions(self.handle))

@@ -135,12 +135,78 @@ struct DevBuf {
     T* as() const { return static_cast<T*>(p); }
 };
 
+// Pinned staging ring of the host -> HBM ingest (registration from pageable host memory):
+// kStageSlots pinned buffers; the host packs chunk k + 1 into one while chunk k's DMA runs from
+// another on the context's copy stream. One Stager per registering thread at a time.
+constexpr int kStageSlots = 3;
+constexpr size_t kStageChunk = size_t(8) << 20;
+struct Stager {
+    char* buf[kStageSlots] = {};
+    size_t cap = 0;
+    hipEvent_t ev[kStageSlots] = {};
+    bool busy[kStageSlots] = {};
+    int next = 0;
+    hipError_t ensure(size_t need) {
+        if (!ev[0])
+            for (auto& e : ev) {
+                hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+                if (r) return r;
+            }
+        if (need <= cap) return hipSuccess;
+        drain();
+        for (auto& b : buf) {
+            if (b) hipHostFree(b);
+            b = nullptr;
+        }
+        cap = 0;
+        for (auto& b : buf) {
+            hipError_t r = hipHostMalloc((void**)&b, need, hipHostMallocDefault);
+            if (r) return r;
+        }
+        cap = need;
+        return hipSuccess;
+    }
+    // the next slot, once its previous DMA has drained
+    hipError_t acquire(int& k) {
+        k = next;
+        next = (next + 1) % kStageSlots;
+        if (busy[k]) {
+            hipError_t r = hipEventSynchronize(ev[k]);
+            if (r) return r;
+            busy[k] = false;
+        }
+        return hipSuccess;
+    }
+    void drain() {
+        for (int k = 0; k < kStageSlots; ++k)
+            if (busy[k]) {
+                hipEventSynchronize(ev[k]);
+                busy[k] = false;
+            }
+    }
+    void release() {
+        drain();
+        for (auto& b : buf)
+            if (b) hipHostFree(b);
+        for (auto& e : ev)
+            if (e) hipEventDestroy(e);
+        *this = Stager{};
+    }
+};
+
 }  // namespace
 
 struct psgd_ctx {
     int32_t device = 0;
     int32_t num_cus = 256;
     hipStream_t stream = nullptr;
+    // Host -> HBM registration copies run on their own stream (they overlap epochs on `stream`
+    // and the caller's packing of the next partition); an epoch waits for them on the device.
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t copy_ev = nullptr;
+    bool copies_pending = false;       // copies enqueued since the last epoch (under mu)
+    std::mutex stage_mu;               // guards `stagers`
+    std::vector<Stager*> stagers;      // idle staging rings
     std::mutex mu;
     std::map<int64_t, Part> parts;
     bool descs_dirty = true;
@@ -229,9 +295,96 @@ int64_t weight_dim(int32_t d, const psgd_params* p) {
     return multinomial(p) ? (int64_t)(p->num_classes - 1) * d : (int64_t)d;
 }
 
+// ---- Host -> HBM ingest (RDD partition -> pinned buffers -> HBM) ----
+
+struct StagerLease {
+    psgd_ctx* ctx;
+    Stager* s;
+    explicit StagerLease(psgd_ctx* c) : ctx(c), s(nullptr) {
+        std::lock_guard<std::mutex> lk(ctx->stage_mu);
+        if (!ctx->stagers.empty()) {
+            s = ctx->stagers.back();
+            ctx->stagers.pop_back();
+        }
+        if (!s) s = new Stager();
+    }
+    ~StagerLease() {
+        s->drain();   // its buffers are reused by the next registration
+        std::lock_guard<std::mutex> lk(ctx->stage_mu);
+        ctx->stagers.push_back(s);
+    }
+};
+
+// True when p is page-locked host memory the device can DMA from directly (psgd_host_alloc, or
+// any hipHostMalloc / hipHostRegister'ed buffer).
+bool is_pinned(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    const hipError_t e = hipPointerGetAttributes(&a, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();   // pageable memory: not an error for us
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+// Copy `bytes` to the device at `dst` on ctx->copy_stream. Pinned sources are DMA'd directly
+// (and waited for: no host pointer outlives the call); pageable ones through the staging ring,
+// in chunks of whole `unit`s: fill(stage, off, len) writes bytes [off, off + len) of the device
+// image into the pinned chunk and returns false to abort (validation failure, message set).
+// Returns with the last chunks' DMA possibly in flight from the library's own buffers.
+template <class Fill>
+int32_t stage_upload(psgd_ctx* ctx, Stager& S, void* dst, size_t bytes, size_t unit, Fill fill) {
+    if (bytes == 0) return PSGD_OK;
+    unit = std::max<size_t>(unit, 1);
+    const size_t chunk = std::max(kStageChunk / unit, size_t(1)) * unit;
+    HIP_TRY(S.ensure(chunk));
+    for (size_t off = 0; off < bytes; off += chunk) {
+        const size_t len = std::min(chunk, bytes - off);
+        int k = 0;
+        HIP_TRY(S.acquire(k));
+        if (!fill(S.buf[k], off, len)) {
+            S.drain();
+            return PSGD_EINVAL;
+        }
+        HIP_TRY(hipMemcpyAsync(static_cast<char*>(dst) + off, S.buf[k], len, hipMemcpyHostToDevice,
+                               ctx->copy_stream));
+        HIP_TRY(hipEventRecord(S.ev[k], ctx->copy_stream));
+        S.busy[k] = true;
+    }
+    return PSGD_OK;
+}
+
+// A contiguous host array to the device: direct DMA when pinned, else staged.
+int32_t upload(psgd_ctx* ctx, Stager& S, void* dst, const void* src, size_t bytes) {
+    if (bytes == 0) return PSGD_OK;
+    if (is_pinned(src)) {
+        HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->copy_stream));
+        return PSGD_OK;
+    }
+    const char* s = static_cast<const char*>(src);
+    return stage_upload(ctx, S, dst, bytes, 1, [&](char* st, size_t off, size_t len) {
+        std::memcpy(st, s + off, len);
+        return true;
+    });
+}
+
+// Wait for the direct (pinned-source) DMAs of this call: the caller may reuse its buffers.
+int32_t finish_direct(psgd_ctx* ctx, bool any_direct) {
+    if (!any_direct) return PSGD_OK;
+    HIP_TRY(hipStreamSynchronize(ctx->copy_stream));
+    return PSGD_OK;
+}
+
 // Allocate per-chain buffers and upload descriptors (ctx->mu held).
 int32_t prepare(psgd_ctx* ctx, int32_t d, int state_vectors, hipStream_t st) {
     const size_t P = ctx->parts.size();
+    if (ctx->copies_pending) {
+        // registration copies still in flight on the copy stream: the epoch waits on the device
+        HIP_TRY(hipEventRecord(ctx->copy_ev, ctx->copy_stream));
+        HIP_TRY(hipStreamWaitEvent(st, ctx->copy_ev, 0));
+        ctx->copies_pending = false;
+    }
     HIP_TRY(ctx->descs.ensure(std::max<size_t>(P, 1) * sizeof(psgd::ChainDesc)));
     HIP_TRY(ctx->w_in.ensure((size_t)std::max(d, 1) * sizeof(double)));
     HIP_TRY(ctx->w_out.ensure(std::max<size_t>(P, 1) * (size_t)std::max(d, 1) * sizeof(double)));
@@ -321,7 +474,11 @@ int32_t psgd_ctx_create(int32_t device, psgd_ctx** out) {
     ctx->device = device;
     ctx->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->copy_ev, hipEventDisableTiming);
     if (e != hipSuccess) {
+        if (ctx->stream) hipStreamDestroy(ctx->stream);
+        if (ctx->copy_stream) hipStreamDestroy(ctx->copy_stream);
         delete ctx;
         return fail(PSGD_EDEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(e));
     }
@@ -333,7 +490,13 @@ int32_t psgd_ctx_destroy(psgd_ctx* ctx) {
     if (!ctx) return PSGD_OK;
     {
         DeviceGuard g(ctx->device);
+        hipStreamSynchronize(ctx->copy_stream);
         hipStreamSynchronize(ctx->stream);
+        for (Stager* s : ctx->stagers) {
+            s->release();
+            delete s;
+        }
+        ctx->stagers.clear();
         for (auto& kv : ctx->parts) free_part(kv.second);
         for (DevBuf* b : {&ctx->descs, &ctx->w_in, &ctx->w_out, &ctx->state, &ctx->rv, &ctx->loss,
                           &ctx->cnt_d, &ctx->cnt, &ctx->steps, &ctx->partial, &ctx->tmp, &ctx->zbuf, &ctx->wf32, &ctx->stamps,
@@ -342,6 +505,8 @@ int32_t psgd_ctx_destroy(psgd_ctx* ctx) {
             b->release();
         if (ctx->ev_begin) hipEventDestroy(ctx->ev_begin);
         if (ctx->ev_end) hipEventDestroy(ctx->ev_end);
+        if (ctx->copy_ev) hipEventDestroy(ctx->copy_ev);
+        hipStreamDestroy(ctx->copy_stream);
         hipStreamDestroy(ctx->stream);
     }
     delete ctx;
@@ -355,10 +520,12 @@ int32_t psgd_register_dense(psgd_ctx* ctx, int64_t part, int64_t n_rows, int32_t
     if (n_rows < 0 || d <= 0) return fail(PSGD_EINVAL, "n_rows must be >= 0 and d > 0");
     if (dtype != PSGD_F64 && dtype != PSGD_F32) return fail(PSGD_EINVAL, "unknown dtype");
     if (n_rows > 0 && (!labels || !x)) return fail(PSGD_EINVAL, "labels/x are null");
-    std::lock_guard<std::mutex> lk(ctx->mu);
     DeviceGuard g(ctx->device);
-    int32_t rc = check_compat(ctx, d, dtype, psgd::kDense);
-    if (rc) return rc;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        int32_t rc = check_compat(ctx, d, dtype, psgd::kDense);
+        if (rc) return rc;
+    }
     const size_t es = dtype_size(dtype);
     const int64_t vec = (int64_t)(16 / es);
     Part p;
@@ -368,21 +535,60 @@ int32_t psgd_register_dense(psgd_ctx* ctx, int64_t part, int64_t n_rows, int32_t
     p.layout = psgd::kDense;
     p.owned = true;
     p.ld = (d + vec - 1) / vec * vec;
+    // The copies run without the context lock (Spark's N task threads register concurrently),
+    // on the copy stream; the partition joins the registry once they are enqueued.
     if (n_rows > 0) {
-        const size_t xbytes = (size_t)n_rows * (size_t)p.ld * es;
+        const size_t row_src = (size_t)d * es, row_dev = (size_t)p.ld * es;
+        const size_t xbytes = (size_t)n_rows * row_dev;
+        struct Undo {
+            psgd_ctx* c; Part* p; bool armed = true;
+            ~Undo() { if (armed) { hipStreamSynchronize(c->copy_stream); free_part(*p); } }
+        } undo{ctx, &p};
         HIP_TRY(hipMalloc(&p.x, xbytes));
         HIP_TRY(hipMalloc((void**)&p.y, (size_t)n_rows * sizeof(double)));
-        if (p.ld != d) HIP_TRY(hipMemsetAsync(p.x, 0, xbytes, ctx->stream));
-        HIP_TRY(hipMemcpy2DAsync(p.x, (size_t)p.ld * es, x, (size_t)d * es, (size_t)d * es,
-                                 (size_t)n_rows, hipMemcpyHostToDevice, ctx->stream));
-        HIP_TRY(hipMemcpyAsync(p.y, labels, (size_t)n_rows * sizeof(double),
-                               hipMemcpyHostToDevice, ctx->stream));
-        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        StagerLease lease(ctx);
+        const bool pinned = is_pinned(x);
+        if (pinned && row_src == row_dev) {
+            HIP_TRY(hipMemcpyAsync(p.x, x, xbytes, hipMemcpyHostToDevice, ctx->copy_stream));
+        } else if (pinned) {
+            HIP_TRY(hipMemsetAsync(p.x, 0, xbytes, ctx->copy_stream));
+            HIP_TRY(hipMemcpy2DAsync(p.x, row_dev, x, row_src, row_src, (size_t)n_rows,
+                                     hipMemcpyHostToDevice, ctx->copy_stream));
+        } else {
+            // rows packed at the device pitch, zero padding included (no device memset)
+            const char* src = static_cast<const char*>(x);
+            int32_t rc = stage_upload(ctx, *lease.s, p.x, xbytes, row_dev, [&](char* st, size_t off, size_t len) {
+                const size_t r0 = off / row_dev, nr = len / row_dev;
+                if (row_src == row_dev) {
+                    std::memcpy(st, src + r0 * row_src, nr * row_src);
+                } else {
+                    for (size_t r = 0; r < nr; ++r) {
+                        std::memcpy(st + r * row_dev, src + (r0 + r) * row_src, row_src);
+                        std::memset(st + r * row_dev + row_src, 0, row_dev - row_src);
+                    }
+                }
+                return true;
+            });
+            if (rc) return rc;
+        }
+        int32_t rc = upload(ctx, *lease.s, p.y, labels, (size_t)n_rows * sizeof(double));
+        if (rc) return rc;
+        rc = finish_direct(ctx, pinned || is_pinned(labels));
+        if (rc) return rc;
+        undo.armed = false;
+    }
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    int32_t rc = check_compat(ctx, d, dtype, psgd::kDense);   // a concurrent registration may differ
+    if (rc) {
+        hipStreamSynchronize(ctx->copy_stream);
+        free_part(p);
+        return rc;
     }
     auto it = ctx->parts.find(part);
     if (it != ctx->parts.end()) free_part(it->second);
     ctx->parts[part] = p;
     ctx->descs_dirty = true;
+    ctx->copies_pending = true;
     return PSGD_OK;
 }
 
@@ -469,20 +675,12 @@ int32_t psgd_register_csr(psgd_ctx* ctx, int64_t part, int64_t n_rows, int32_t d
     }
     const int64_t nnz = rp[(size_t)n_rows];
     if (nnz > 0 && (!col || !val)) return fail(PSGD_EINVAL, "col/val are null");
-    for (int64_t r = 0; r < n_rows; ++r) {
-        for (int64_t k = rp[(size_t)r]; k < rp[(size_t)r + 1]; ++k) {
-            const int32_t c = col[base + k];
-            if (c < 0 || c >= d)
-                return fail(PSGD_EINVAL, "requirement failed: column index " + std::to_string(c) +
-                                             " out of range [0, " + std::to_string(d) + ")");
-            if (k > rp[(size_t)r] && c <= col[base + k - 1])
-                return fail(PSGD_EINVAL, "column indices must be strictly increasing within a row");
-        }
-    }
-    std::lock_guard<std::mutex> lk(ctx->mu);
     DeviceGuard g(ctx->device);
-    int32_t rc = check_compat(ctx, d, dtype, psgd::kCsr);
-    if (rc) return rc;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        int32_t rc = check_compat(ctx, d, dtype, psgd::kCsr);
+        if (rc) return rc;
+    }
     const size_t es = dtype_size(dtype);
     Part p;
     p.n_rows = n_rows;
@@ -492,27 +690,108 @@ int32_t psgd_register_csr(psgd_ctx* ctx, int64_t part, int64_t n_rows, int32_t d
     p.owned = true;
     for (int64_t r = 0; r < n_rows; ++r)
         p.max_nnz = std::max<int64_t>(p.max_nnz, rp[(size_t)r + 1] - rp[(size_t)r]);
+    // Copies without the context lock, on the copy stream (see psgd_register_dense). The column
+    // indices are validated chunk by chunk as they are packed, so a pageable partition is read
+    // once; a failure drains the copies and frees the partition's buffers.
     if (n_rows > 0) {
+        struct Undo {
+            psgd_ctx* c; Part* p; bool armed = true;
+            ~Undo() { if (armed) { hipStreamSynchronize(c->copy_stream); free_part(*p); } }
+        } undo{ctx, &p};
         HIP_TRY(hipMalloc((void**)&p.row_ptr, rp.size() * sizeof(int64_t)));
         HIP_TRY(hipMalloc((void**)&p.y, (size_t)n_rows * sizeof(double)));
-        HIP_TRY(hipMemcpyAsync(p.row_ptr, rp.data(), rp.size() * sizeof(int64_t),
-                               hipMemcpyHostToDevice, ctx->stream));
-        HIP_TRY(hipMemcpyAsync(p.y, labels, (size_t)n_rows * sizeof(double),
-                               hipMemcpyHostToDevice, ctx->stream));
+        StagerLease lease(ctx);
+        int32_t rc = upload(ctx, *lease.s, p.row_ptr, rp.data(), rp.size() * sizeof(int64_t));
+        if (rc) return rc;
+        rc = upload(ctx, *lease.s, p.y, labels, (size_t)n_rows * sizeof(double));
+        if (rc) return rc;
+        bool direct = is_pinned(labels);
         if (nnz > 0) {
             HIP_TRY(hipMalloc((void**)&p.col, (size_t)nnz * sizeof(int32_t)));
             HIP_TRY(hipMalloc(&p.x, (size_t)nnz * es));
-            HIP_TRY(hipMemcpyAsync(p.col, col + base, (size_t)nnz * sizeof(int32_t),
-                                   hipMemcpyHostToDevice, ctx->stream));
-            HIP_TRY(hipMemcpyAsync(p.x, static_cast<const char*>(val) + (size_t)base * es,
-                                   (size_t)nnz * es, hipMemcpyHostToDevice, ctx->stream));
+            const int32_t* cs = col + base;
+            // entries [k0, k1): in range, strictly increasing inside a row
+            int64_t row = 0;
+            auto check = [&](int64_t k0, int64_t k1) -> bool {
+                for (int64_t k = k0; k < k1; ++k) {
+                    while (rp[(size_t)row + 1] <= k) ++row;
+                    const int32_t c = cs[k];
+                    if (c < 0 || c >= d) {
+                        fail(PSGD_EINVAL, "requirement failed: column index " + std::to_string(c) +
+                                              " out of range [0, " + std::to_string(d) + ")");
+                        return false;
+                    }
+                    if (k > rp[(size_t)row] && c <= cs[k - 1]) {
+                        fail(PSGD_EINVAL, "column indices must be strictly increasing within a row");
+                        return false;
+                    }
+                }
+                return true;
+            };
+            if (is_pinned(cs)) {
+                if (!check(0, nnz)) return PSGD_EINVAL;
+                HIP_TRY(hipMemcpyAsync(p.col, cs, (size_t)nnz * sizeof(int32_t), hipMemcpyHostToDevice,
+                                       ctx->copy_stream));
+                direct = true;
+            } else {
+                rc = stage_upload(ctx, *lease.s, p.col, (size_t)nnz * sizeof(int32_t), sizeof(int32_t),
+                                  [&](char* st, size_t off, size_t len) {
+                                      const int64_t k0 = (int64_t)(off / 4), k1 = (int64_t)((off + len) / 4);
+                                      if (!check(k0, k1)) return false;
+                                      std::memcpy(st, cs + k0, len);
+                                      return true;
+                                  });
+                if (rc) return rc;
+            }
+            const char* vs = static_cast<const char*>(val) + (size_t)base * es;
+            direct = direct || is_pinned(vs);
+            rc = upload(ctx, *lease.s, p.x, vs, (size_t)nnz * es);
+            if (rc) return rc;
         }
-        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        rc = finish_direct(ctx, direct);
+        if (rc) return rc;
+        undo.armed = false;
+    }
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    int32_t rc = check_compat(ctx, d, dtype, psgd::kCsr);   // a concurrent registration may differ
+    if (rc) {
+        hipStreamSynchronize(ctx->copy_stream);
+        free_part(p);
+        return rc;
     }
     auto it = ctx->parts.find(part);
     if (it != ctx->parts.end()) free_part(it->second);
     ctx->parts[part] = p;
     ctx->descs_dirty = true;
+    ctx->copies_pending = true;
+    return PSGD_OK;
+}
+
+int32_t psgd_host_alloc(psgd_ctx* ctx, int64_t bytes, void** out) {
+    if (!ctx || !out) return fail(PSGD_EINVAL, "ctx/out is null");
+    *out = nullptr;
+    if (bytes <= 0) return fail(PSGD_EINVAL, "bytes must be > 0");
+    DeviceGuard g(ctx->device);
+    hipError_t e = hipHostMalloc(out, (size_t)bytes, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        *out = nullptr;
+        return fail(PSGD_ENOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    }
+    return PSGD_OK;
+}
+
+int32_t psgd_host_free(psgd_ctx* ctx, void* p) {
+    if (!ctx) return fail(PSGD_EINVAL, "ctx is null");
+    if (!p) return PSGD_OK;
+    DeviceGuard g(ctx->device);
+    HIP_TRY(hipHostFree(p));
+    return PSGD_OK;
+}
+
+int32_t psgd_register_wait(psgd_ctx* ctx) {
+    if (!ctx) return fail(PSGD_EINVAL, "ctx is null");
+    DeviceGuard g(ctx->device);
+    HIP_TRY(hipStreamSynchronize(ctx->copy_stream));
     return PSGD_OK;
 }
 
