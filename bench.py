@@ -41,7 +41,7 @@ CSR_NNZ = {"c4": 94, "c5": 100}  # nonzeros per row (c4: rcv1's mean; c5: SURVEY
 REG = {"c5": 1e-6}                # SquaredL2 regParam (c5); others: Simple updater
 # secondary lines: rows per GPU (0 = the workload's own; c5's full 125M-row shard takes minutes)
 SECONDARY_ROWS = {"c5": 20_000_000}
-DEFAULT_SECONDARY = "c3:f64,c3:f32,c2:f64,c1:f64,c4:f32"
+DEFAULT_SECONDARY = "c3:f64,c3:f32,c2:f64,c1:f64,c4:f32,c5:f32,c2:f32:adagrad,c2:f32:adam"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
@@ -87,7 +87,11 @@ def kernel_name(variant):
     if 600 <= variant < 700:
         return (f"chain_sparse_lds (fp32 CSR chain, weights LDS-resident [tail past ~160 KiB: L2-resident, "
                 f"gathered {8 if variant >= 610 else 4} samples ahead with an LDS feature-tag correction])")
-    if 410 <= variant < 500:
+    if 420 <= variant < 450:
+        sk = {42: 8, 43: 4, 44: 16}[variant // 10]
+        return (f"chain_sparse_spec (fp32 CSR chain, weights HBM-resident, gathers {sk} samples "
+                "ahead, correction entries by binary search in the window rows)")
+    if 410 <= variant < 420:
         return ("chain_sparse_spec (fp32 CSR chain, weights L2/MALL-resident, gathers 8 samples "
                 "ahead with an LDS feature-tag correction)")
     if 400 <= variant < 410:
@@ -106,12 +110,14 @@ def parse():
     ap.add_argument("--compute", default="f32", choices=["f32", "f64"])
     ap.add_argument("--rows", type=int, default=0, help="override rows per GPU (testing)")
     ap.add_argument("--features", type=int, default=0, help="override d (experiments; not a BASELINE config)")
+    ap.add_argument("--chains", type=int, default=0, help="override chains per GPU (experiments; not a BASELINE config)")
     ap.add_argument("--fraction", type=float, default=1.0,
                     help="miniBatchFraction: batch i = RDD.sample(false, f, 42 + i) per partition")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--secondary", default=DEFAULT_SECONDARY,
-                    help="comma list of workload[:compute] measured after the headline (1 GPU only; '' = none)")
+                    help="comma list of workload[:compute[:updater]] measured after the headline (1 GPU only; '' = none)")
+    ap.add_argument("--updater", default="", help="another SGDUpdater for the headline workload (experiments)")
     ap.add_argument("--prewarm-s", type=float, default=1.0,
                     help="untimed epochs for this long before the warmup steps (GPU clock ramp)")
     return ap.parse_args()
@@ -221,7 +227,7 @@ def cpu_baseline(grad, d, P, step, budget_s, seed=7, csr_nnz=0):
 
 
 def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, rows, fraction,
-                 steps, warmup, prewarm_s, features=0):
+                 steps, warmup, prewarm_s, features=0, chains=0, updater=""):
     """One workload: synthetic shard in HBM, prewarm, W warmup steps, K timed steps (barrier +
     synchronize on both sides, max over ranks). Returns the measurement as a dict."""
     import numpy as np
@@ -231,6 +237,9 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
     if features:
         d = features
         cfg_name += f" [d overridden: {d}]"
+    if chains:
+        P = chains
+        cfg_name += f" [chains overridden: {P}]"
     csr = workload in CSR_NNZ
     if csr:
         rp, col, val, y, offs = make_csr_shard(torch, dev, n, d, P, grad, sdt, 1000 + rank,
@@ -255,6 +264,9 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
             "hinge": pkg.HingeGradient}[grad]()
     reg = REG.get(workload, 0.0)
     ucls = pkg.SquaredL2SGDUpdater() if reg > 0 else pkg.SimpleSGDUpdater()
+    if updater:   # the workload with another SGDUpdater plugin (UPD.scala:120-286)
+        ucls = {"l1": pkg.L1SGDUpdater, "adagrad": pkg.AdaGradSGDUpdater, "adam": pkg.AdamSGDUpdater,
+                "simple": pkg.SimpleSGDUpdater, "squared_l2": pkg.SquaredL2SGDUpdater}[updater]()
     params = pkg.make_params(gcls, ucls, step, reg, fraction, 0.0, compute)
     w = engine.weights(np.zeros(d))
     stream = engine.stream  # the engine's kernels and copies all run on this stream
@@ -348,7 +360,7 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
         "value": value, "ms_per_step": elapsed / steps * 1e3, "dtype": compute, "loss": loss,
         "config": {"workload": f"{workload}: {cfg_name}", "rows_per_gpu": n, "d": d,
                    "chains_per_gpu": P, "storage": sdt, "gradient": grad,
-                   "updater": "squared_l2" if reg > 0 else "simple", "reg_param": reg,
+                   "updater": updater or ("squared_l2" if reg > 0 else "simple"), "reg_param": reg,
                    "step_size": step, "convergence_tol": 0.0, "mini_batch_fraction": fraction,
                    "parallelism": f"dp{world} (chains sharded, RCCL all-gather + fold per epoch)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -399,7 +411,8 @@ def main():
     torch.cuda.set_device(dev)
 
     res = run_workload(torch, dist, pkg, dev, rank, world, local, args.workload, args.compute,
-                       args.rows, args.fraction, args.steps, args.warmup, args.prewarm_s, args.features)
+                       args.rows, args.fraction, args.steps, args.warmup, args.prewarm_s, args.features,
+                       args.chains, args.updater)
     grad, d, P, step, csr = res.pop("_meta")
     res.pop("loss")
     out = {
@@ -419,11 +432,11 @@ def main():
     if secondary:
         out["secondary"] = []
     for spec in secondary:
-        wl, _, comp = spec.partition(":")
+        wl, comp, upd = (spec.split(":") + ["", ""])[:3]
         torch.cuda.empty_cache()
         r = run_workload(torch, dist, pkg, dev, rank, world, local, wl, comp or "f32",
                          SECONDARY_ROWS.get(wl, 0), 1.0, args.steps, args.warmup,
-                         min(args.prewarm_s, 0.5))
+                         min(args.prewarm_s, 0.5), updater=upd)
         r.pop("_meta")
         r["samples_per_s"] = r.pop("value")
         r["loss"] = float(r["loss"])

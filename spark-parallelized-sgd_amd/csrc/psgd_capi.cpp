@@ -211,6 +211,7 @@ struct psgd_ctx {
     std::map<int64_t, Part> parts;
     bool descs_dirty = true;
     DevBuf descs, w_in, w_out, state, rv, loss, cnt_d, cnt, steps, partial, tmp, watchdog, zbuf, wf32, stamps;
+    DevBuf walpha, wnsq0;                // the fp32 CSR chains' weight scale and ||float(w_in)||^2
     DevBuf sdescs, srows, sys, xstate;   // sampled epochs (miniBatchFraction < 1)
     double steps_value = NAN;
     int64_t steps_n = 0;
@@ -499,7 +500,7 @@ int32_t psgd_ctx_destroy(psgd_ctx* ctx) {
         ctx->stagers.clear();
         for (auto& kv : ctx->parts) free_part(kv.second);
         for (DevBuf* b : {&ctx->descs, &ctx->w_in, &ctx->w_out, &ctx->state, &ctx->rv, &ctx->loss,
-                          &ctx->cnt_d, &ctx->cnt, &ctx->steps, &ctx->partial, &ctx->tmp, &ctx->zbuf, &ctx->wf32, &ctx->stamps,
+                          &ctx->cnt_d, &ctx->cnt, &ctx->steps, &ctx->partial, &ctx->tmp, &ctx->zbuf, &ctx->wf32, &ctx->stamps, &ctx->walpha, &ctx->wnsq0,
                           &ctx->sdescs, &ctx->srows, &ctx->sys, &ctx->xstate,
                           &ctx->watchdog})
             b->release();
@@ -912,12 +913,19 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
     L.zstride = 0;
     L.wf32 = nullptr;
     L.wstride = 0;
+    L.walpha = nullptr;
+    L.wnsq0 = nullptr;
     if (layout == psgd::kCsr && params->compute_dtype == PSGD_F32) {
         // fp32 working weights of the CSR kernels (one d-vector per chain, HBM/L2-resident, and
         // 128 + 1024 floats the kernels' masked-off lanes load from / store to)
-        L.wstride = (int64_t)d + 128 + 1024;
+        // (rows 256-byte aligned: the epoch's init kernel stores 16-byte vectors)
+        L.wstride = ((int64_t)d + 128 + 1024 + 63) / 64 * 64;
         HIP_TRY(ctx->wf32.ensure((size_t)P * (size_t)L.wstride * sizeof(float)));
+        HIP_TRY(ctx->walpha.ensure((size_t)P * sizeof(double)));
+        HIP_TRY(ctx->wnsq0.ensure(sizeof(double)));
         L.wf32 = ctx->wf32.as<float>();
+        L.walpha = ctx->walpha.as<double>();
+        L.wnsq0 = ctx->wnsq0.as<double>();
     }
     if (params->gradient == PSGD_GRADIENT_LOGISTIC && params->compute_dtype == PSGD_F32 &&
         layout == psgd::kDense) {
@@ -987,7 +995,12 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         if (e) return fail(PSGD_EDEVICE, std::string("chain kernel launch failed: ") +
                                              hipGetErrorString((hipError_t)e));
     }
-    int e = psgd::launch_fold(L.w_out, dw, L.rv, L.loss, L.cnt_d, 1, P, dw, d_partial, L.watchdog, st);
+    // the fp32 CSR kernels (variants 400-699) leave each chain's weights in L.wf32 (w = alpha v)
+    const bool from_wf32 = !sample_empty && L.wf32 && ctx->last_variant >= 400 && ctx->last_variant < 700;
+    int e = from_wf32
+                ? psgd::launch_fold_f32(L.wf32, L.wstride, L.walpha, L.rv, L.loss, L.cnt_d, P, dw, d_partial,
+                                        L.watchdog, st)
+                : psgd::launch_fold(L.w_out, dw, L.rv, L.loss, L.cnt_d, 1, P, dw, d_partial, L.watchdog, st);
     if (e) return fail(PSGD_EDEVICE, "fold kernel launch failed");
     if (d_chain_counts)
         HIP_TRY(hipMemcpyAsync(d_chain_counts, L.cnt, (size_t)P * sizeof(int64_t),

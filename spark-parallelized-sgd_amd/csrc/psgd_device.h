@@ -145,6 +145,8 @@ __device__ __forceinline__ double m_fabs(double x) { return __builtin_fabs(x); }
 __device__ __forceinline__ float m_fabs(float x) { return __builtin_fabsf(x); }
 __device__ __forceinline__ float m_sqrt(float x) { return sqrtf(x); }
 __device__ __forceinline__ double m_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
+__device__ __forceinline__ double m_pow(double a, double b) { return pow(a, b); }
+__device__ __forceinline__ float m_pow(float a, float b) { return powf(a, b); }
 __device__ __forceinline__ float m_fma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 
 // java.lang.Math.max(a, b): NaN if either is NaN.
@@ -221,6 +223,37 @@ __device__ __forceinline__ float gather_sc1(const float* p) {
 }
 __device__ __forceinline__ void store_f32(float* p, float v) {
     asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");
+}
+
+// fp32 CSR chains with SquaredL2 track ||v||^2 as they update (regVal needs ||w|| after the
+// chain's last sample, PSGD.scala:257, and an O(d) pass per chain over 2^22 features is what the
+// sample stream cannot afford): the change of one coordinate, exact products of floats in f64.
+__device__ __forceinline__ double nsq_delta(float w_old, float w_new) {
+    const double a = double(w_old), b = double(w_new);
+    return b * b - a * a;
+}
+
+// The end of an fp32 CSR chain: its weights stay in L.wf32 (w = alpha v, folded by
+// launch_fold_f32), regVal = 0.5 lambda ||alpha v||^2 (UPD.scala:176-180) from the tracked norm.
+template <bool L2>
+__device__ __forceinline__ void sparse_chain_out(const ChainLaunch& L, const KParams& kp, int chain,
+                                                 int lane, double alpha, double dnsq, double loss_sum,
+                                                 int64_t count) {
+    double rv = 0.0;
+    if constexpr (L2) {
+        const double nsq = *L.wnsq0 + wave_sum(dnsq);
+        if (count > 0) {
+            const double nrm = sqrt(alpha * alpha * nsq);
+            rv = 0.5 * kp.reg * nrm * nrm;
+        }
+    }
+    if (lane == 0) {
+        L.walpha[chain] = alpha;
+        L.rv[chain] = rv;
+        L.loss[chain] = loss_sum;
+        L.cnt[chain] = count;
+        L.cnt_d[chain] = double(count);
+    }
 }
 
 template <int... Is, typename F>

@@ -53,6 +53,11 @@ struct ChainLaunch {
     int64_t zstride;
     float* wf32;             // [n_chains * wstride] fp32 working weights (CSR fp32 kernel)
     int64_t wstride;
+    // CSR fp32 kernels: the chain's weights are w = walpha[chain] * wf32[chain] (SquaredL2's
+    // alpha-scaled form; 1 otherwise), folded straight from wf32 (launch_fold_f32); wnsq0 =
+    // ||float(w_in)||^2, the start of the chain's incrementally tracked ||v||^2.
+    double* walpha;          // [n_chains]
+    double* wnsq0;           // [1]
 };
 
 // Diagnostic builds (-DPSGD_STAMPS, tools/chain_bench.hip) count s_memtime cycles per wave.
@@ -86,6 +91,10 @@ int launch_logistic_loss64(const ChainLaunch& L, int n_chains, hipStream_t strea
 int launch_fold(const double* w, int64_t w_stride, const double* rv, const double* loss,
                 const double* cnt, int64_t s_stride, int n, int d, double* out,
                 const int* watchdog, hipStream_t stream);
+// The combiner over the CSR fp32 kernels' outputs: w_p = walpha[p] * double(wf32[p][i]).
+int launch_fold_f32(const float* wf32, int64_t wstride, const double* walpha, const double* rv,
+                    const double* loss, const double* cnt, int n, int d, double* out,
+                    const int* watchdog, hipStream_t stream);
 int launch_sq_terms(const double* a, const double* b, int d, double* out2, hipStream_t stream);
 int launch_steps(double step, int64_t n, double* steps, hipStream_t stream);
 // The fp32 CSR kernel (psgd_sparse.hip): weights as fp32 vectors in HBM (L.wf32).

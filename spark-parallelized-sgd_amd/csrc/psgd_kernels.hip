@@ -75,6 +75,18 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, Ri
         }
     }
 
+    // AdaGrad / Adam status (UPD.scala:193-286) in registers beside the weights, laid out as w:
+    // ua = the squared-gradient accumulator (AdaGrad) or v (Adam), ub = r (Adam). The reference
+    // starts each chain's status at None (`updater.initStatus`, PSGD.scala:246): the first sample
+    // takes the `None` branch.
+    constexpr bool STATE_A = UPD == U_ADAGRAD || UPD == U_ADAM;
+    constexpr bool STATE_B = UPD == U_ADAM;
+    T2 ua[STATE_A ? E2 : 1], ub[STATE_B ? E2 : 1];
+#pragma unroll
+    for (int e = 0; e < (STATE_A ? E2 : 1); ++e) ua[e] = T2{T(0), T(0)};
+#pragma unroll
+    for (int e = 0; e < (STATE_B ? E2 : 1); ++e) ub[e] = T2{T(0), T(0)};
+
     // Row buffers: two register copies (ping-pong) so row t+1's LDS reads are in flight while
     // sample t computes.
     T2 xb[2][E2];
@@ -184,11 +196,38 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, Ri
 
         const T a = -s;
         T2 dsq2 = T2{T(0), T(0)}, nsq2 = T2{T(0), T(0)};
+        // Adam's per-sample scalars (UPD.scala:258-262): iter = j, lr = s / (1 - beta^iter)
+        const bool first = t == 0;
+        const T iter = T(t + 1);
+        T al = T(0);
+        if constexpr (UPD == U_ADAM) al = -(s / (T(1) - m_pow(T(kp.beta), iter)));
 #pragma unroll
         for (int e = 0; e < E2; ++e) {
             const T2 old = w[e];
             T2 nw;
-            if constexpr (UPD == U_SQUARED_L2) {
+            if constexpr (UPD == U_ADAGRAD) {
+                // accum = None ? g*g : accum + g*g; w += -s * (g / sqrt(accum + 1.0))
+                const T2 g = mult * x[e];
+                const T2 acc2 = first ? g * g : ua[e] + g * g;
+                ua[e] = acc2;
+                nw.x = old.x + a * (g.x / m_sqrt(acc2.x + T(1)));
+                nw.y = old.y + a * (g.y / m_sqrt(acc2.y + T(1)));
+            } else if constexpr (UPD == U_ADAM) {
+                // the reference's variant, literally: v = beta v + (1-beta) g,
+                // r = gamma r + (1-gamma) g^2, fix1 = sqrt(1 - r^iter) + eps, w += -lr * v / fix1
+                const T beta = T(kp.beta), gamma = T(kp.gamma);
+                const T2 g = mult * x[e];
+                const T2 sq = g * g;
+                T2 v, r;
+                if (first) { v = g * (T(1) - beta); r = sq * (T(1) - gamma); }
+                else { v = ua[e] * beta + g * (T(1) - beta); r = ub[e] * gamma + sq * (T(1) - gamma); }
+                ua[e] = v;
+                ub[e] = r;
+                const T fx = m_sqrt(T(1) - m_pow(r.x, iter)) + T(kp.eps);
+                const T fy = m_sqrt(T(1) - m_pow(r.y, iter)) + T(kp.eps);
+                nw.x = old.x + al * (v.x / fx);
+                nw.y = old.y + al * (v.y / fy);
+            } else if constexpr (UPD == U_SQUARED_L2) {
                 const T c = T(1) - s * T(kp.reg);
                 nw = old * c;                       // brzWeights :*= (1 - s*lambda)
                 nw = nw + a * (mult * x[e]);        // axpy(-s, grad, w)
@@ -585,6 +624,49 @@ __global__ void fold_kernel(const double* __restrict__ w, int64_t w_stride,
     }
 }
 
+// The same combiner over the fp32 CSR chains' weights, w_p = walpha[p] * double(v_p[i]) -- the
+// value those chains once wrote to w_out, so the fold's arithmetic is unchanged; reading the
+// fp32 vectors directly saves the O(P d) f64 write and re-read (C5: 2^22 features x 1024 chains).
+__global__ void fold_f32_kernel(const float* __restrict__ v, int64_t v_stride,
+                                const double* __restrict__ alpha, const double* __restrict__ rv,
+                                const double* __restrict__ loss, const double* __restrict__ cnt,
+                                int n, int d, double* __restrict__ out, const int* __restrict__ watchdog) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < d) {
+        double acc = alpha[0] * double(v[i]);
+        double c1 = cnt[0];
+#pragma unroll 16
+        for (int p = 1; p < n; ++p) {
+            const double c2 = cnt[p];
+            acc = (acc * c1 + alpha[p] * double(v[p * v_stride + i]) * c2) / (c1 + c2);
+            c1 = c1 + c2;
+        }
+        out[i] = acc;
+    } else if (i == d) {
+        double r = rv[0], l = loss[0], c1 = cnt[0];
+        for (int p = 1; p < n; ++p) {
+            const double c2 = cnt[p];
+            r = (r * c1 + rv[p] * c2) / (c1 + c2);
+            l = l + loss[p];
+            c1 = c1 + c2;
+        }
+        out[d] = r;
+        out[d + 1] = l;
+        out[d + 2] = (watchdog && *watchdog) ? __builtin_nan("") : c1;
+    }
+}
+
+int launch_fold_f32(const float* wf32, int64_t wstride, const double* walpha, const double* rv,
+                    const double* loss, const double* cnt, int n, int d, double* out,
+                    const int* watchdog, hipStream_t stream) {
+    if (n <= 0) return -1;
+    const int threads = 256;
+    const int blocks = (d + 1 + threads - 1) / threads;
+    hipLaunchKernelGGL(fold_f32_kernel, dim3(blocks), dim3(threads), 0, stream, wf32, wstride, walpha,
+                       rv, loss, cnt, n, d, out, watchdog);
+    return (int)hipGetLastError();
+}
+
 // sum((a-b)^2) and sum(b^2) (a may be null: then sum(b^2) and sum(|b|)) -- one block, fixed
 // reduction tree, deterministic.
 __global__ __launch_bounds__(256) void sq_terms_kernel(const double* __restrict__ a,
@@ -723,6 +805,11 @@ static int dispatch_layout(const ChainLaunch& L, const KParams& kp, int layout, 
             if (compute == 1) return dispatch_nv<S, float, GRAD, UPD, CONV>(L, kp, min_ld, max_ld, lds, st, variant);
             return dispatch_nv<S, double, GRAD, UPD, CONV>(L, kp, min_ld, max_ld, lds, st, variant);
         }
+    } else {
+        // AdaGrad / Adam in the fp32 throughput mode: weights and status in registers (the fp64
+        // parity mode keeps chain_general, status in HBM)
+        if (layout == kDense && compute == 1 && max_ld <= 8 * 64 * VEC)
+            return dispatch_nv<S, float, GRAD, UPD, CONV>(L, kp, min_ld, max_ld, lds, st, variant);
     }
     if (layout == kDense) return launch_gen<S, kDense, GRAD, UPD, CONV>(L, kp, st, variant);
     return launch_gen<S, kCsr, GRAD, UPD, CONV>(L, kp, st, variant);

@@ -34,7 +34,6 @@ __global__ __launch_bounds__(64) void chain_sparse(ChainLaunch L, KParams kp) {
     const int lane = threadIdx.x;
     const int chain = blockIdx.x;
     const ChainDesc dsc = L.descs[chain];
-    const int d = kp.d;
     const int64_t n = dsc.n_rows;
     const gptr<S> X = as_global(reinterpret_cast<const S*>(dsc.x));
     const gptr<int32_t> COL = as_global(dsc.col);
@@ -42,14 +41,11 @@ __global__ __launch_bounds__(64) void chain_sparse(ChainLaunch L, KParams kp) {
     const gptr<double> Y = as_global(dsc.y);
     const gptr<double> STEPS = as_global(L.steps);
     const gptr<int32_t> RIDX = dsc.rows ? as_global(dsc.rows) : nullptr;   // sampled epoch
-    float* V = L.wf32 + (int64_t)chain * L.wstride;
+    float* V = L.wf32 + (int64_t)chain * L.wstride;   // = float(w_in) (wf32_init_kernel)
     const gmut<float> VW = as_global_mut(V);
 
-    for (int i = lane; i < d; i += 64) VW[i] = float(as_global(L.w_in)[i]);
-    // the chain's gathers below are loads of these addresses from the same wave
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
     double alpha = 1.0;      // SquaredL2: w = alpha * v
+    double dnsq = 0.0;       // SquaredL2: this lane's part of ||v||^2 - ||v_0||^2
     double loss_sum = 0.0;
     float loss_blk = 0.0f;
     int64_t count = 0;
@@ -121,12 +117,16 @@ __global__ __launch_bounds__(64) void chain_sparse(ChainLaunch L, KParams kp) {
         count += 1;
         if (c != 0.0f) {
             const float cv = L2 ? float(double(c) / alpha) : c;
-            if (a0) VW[c0] = __builtin_fmaf(cv, x0, w0);
-            if (a1) VW[c1] = __builtin_fmaf(cv, x1, w1);
+            const float nv0 = __builtin_fmaf(cv, x0, w0), nv1 = __builtin_fmaf(cv, x1, w1);
+            if (a0) VW[c0] = nv0;
+            if (a1) VW[c1] = nv1;
+            if constexpr (L2) dnsq += nsq_delta(w0, nv0) + nsq_delta(w1, nv1);
             for (int64_t k = kb + 128 + lane; k < ke; k += 64) {
                 const int32_t j = COL[k];
-                VW[j] = __builtin_fmaf(cv, float(X[k]), __hip_atomic_load(&V[j], __ATOMIC_RELAXED,
-                                                                          __HIP_MEMORY_SCOPE_AGENT));
+                const float wj = __hip_atomic_load(&V[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const float nj = __builtin_fmaf(cv, float(X[k]), wj);
+                VW[j] = nj;
+                if constexpr (L2) dnsq += nsq_delta(wj, nj);
             }
         }
         kb = kb1; ke = ke1; kb1 = kb2; ke1 = ke2;
@@ -136,56 +136,39 @@ __global__ __launch_bounds__(64) void chain_sparse(ChainLaunch L, KParams kp) {
     if constexpr (GRAD == G_LEAST_SQUARES) loss_sum = loss_sum / 2.0;
 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // the chain's weights (w = alpha v) and regVal of its last update (PSGD.scala:257)
-    double nsq = 0.0;
-    double* wo = L.w_out + (int64_t)chain * d;
-    for (int i = lane; i < d; i += 64) {
-        const double wv = alpha * double(__hip_atomic_load(&V[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        wo[i] = wv;
-        if constexpr (L2) nsq += wv * wv;
-    }
-    double rv = 0.0;
-    if constexpr (L2) {
-        nsq = wave_sum(nsq);
-        if (count > 0) {
-            const double nrm = sqrt(nsq);
-            rv = 0.5 * kp.reg * nrm * nrm;
-        }
-    }
-    if (lane == 0) {
-        L.rv[chain] = rv;
-        L.loss[chain] = loss_sum;
-        L.cnt[chain] = count;
-        L.cnt_d[chain] = double(count);
-    }
+    sparse_chain_out<L2>(L, kp, chain, lane, alpha, dnsq, loss_sum, count);
 }
 
 // ------------------------------------------------------------------------------------------
 // chain_sparse_spec: the same chain with the gathers issued SK samples ahead (rows of <= 128
-// non-zeros, d small enough for a per-feature tag table in LDS, 47,236 at rcv1 shape).
+// non-zeros).
 //
 // A gather for row u issued during sample u-SK does not see the stores of rows u-SK .. u-1
 // (issued after it). A helper wave finds, for every entry of row u, the latest of those rows
-// that has the same feature: it keeps tagpos[j] = (row & 255) << 8 | entry of the last row that
-// touched feature j; an entry from outside the window is ignored, and a row's tags are cleared
-// before its LDS slot is reused (so an 8-bit row tag never aliases). The chain wave replaces such a gathered value by
-// that row's new value (kept in LDS) -- exactly the value the reference's sequential update
-// would read. Waves:
+// that has the same feature, in one of two ways:
+//   * tag table (BS = false; d small enough for 2 bytes per feature in LDS, 47,236 at rcv1
+//     shape): tagpos[j] = (row & 255) << 8 | entry of the last row that touched feature j; an
+//     entry from outside the window is ignored, and a row's tags are cleared before its LDS
+//     slot is reused (so an 8-bit row tag never aliases);
+//   * binary search (BS = true; any d -- 2^22 in BASELINE config 5): a row's column indices
+//     are strictly increasing, so each entry is looked up in each of the SK window rows' slots
+//     (7 halvings + 1 compare over <= 128 entries); no per-feature state at all.
+// The chain wave replaces such a gathered value by that row's new value (kept in LDS) --
+// exactly the value the reference's sequential update would read. Waves:
 //   wave 0 (chain)  per sample t: waits for row t's gather (issued SK samples earlier; a fixed
 //                   count of VMEM instructions per sample makes it s_waitcnt vmcnt(4 SK - 2)),
 //                   corrects it, dot + wave reduction + coefficient, issues the gather of row
 //                   t + SK, stores the row's new weights (to HBM and to its LDS slot);
 //   wave 1 (helper) loads the rows (64 row pointers / labels / steps per batch, entries of 8
-//                   rows per round trip) into an R-slot LDS ring with their correction entries.
+//                   rows per round trip) into an SR-slot LDS ring with their correction entries.
+// The chain's weights start as float(w_in) (wf32_init_kernel) and stay in L.wf32.
 // ------------------------------------------------------------------------------------------
-constexpr int SK = 8;             // speculation depth (samples)
-constexpr int SR = 32;            // LDS row slots
 constexpr int SCAP = 128;         // entries per row (two per lane)
 // The chain at sample t needs row t + SK staged; the helper stages 8-row groups and may reuse
 // the slot of row u - SR once the chain is done with row u - SR + SK: it can always stage the
 // group holding row t + SK if SR >= 2 SK + 8.
-static_assert(SR >= 2 * SK + 8, "ring too small for the speculation depth");
-static_assert((SR & (SR - 1)) == 0, "slot index by mask");
+template <int SK, int SR>
+constexpr bool spec_ring_ok() { return SR >= 2 * SK + 8 && (SR & (SR - 1)) == 0 && 4 * SK - 2 <= 63; }
 
 struct SpecHeader {
     unsigned ready;   // rows staged by the helper
@@ -203,8 +186,9 @@ struct SpecSlot {
     double y, s;
 };
 
-template <typename S, int GRAD, int UPD>
+template <typename S, int GRAD, int UPD, int SK, int SR, bool BS>
 __global__ __launch_bounds__(128) void chain_sparse_spec(ChainLaunch L, KParams kp) {
+    static_assert(spec_ring_ok<SK, SR>(), "ring too small for the speculation depth");
     constexpr bool L2 = UPD == U_SQUARED_L2;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     SpecHeader* hdr = reinterpret_cast<SpecHeader*>(smem);
@@ -218,11 +202,9 @@ __global__ __launch_bounds__(128) void chain_sparse_spec(ChainLaunch L, KParams 
     const int64_t n = dsc.n_rows;
     float* V = L.wf32 + (int64_t)chain * L.wstride;   // [d] weights + [128] dummy targets
 
-    for (int i = threadIdx.x; i < d; i += blockDim.x) tagpos[i] = 0xFFFF;
+    if constexpr (!BS)
+        for (int i = threadIdx.x; i < d; i += blockDim.x) tagpos[i] = 0xFFFF;
     if (threadIdx.x == 0) { hdr->ready = 0; hdr->done = 0; hdr->stop = 0; }
-    if (wave == 0) {
-        for (int i = lane; i < d; i += 64) as_global_mut(V)[i] = float(as_global(L.w_in)[i]);
-    }
     __syncthreads();
 
     uint64_t st_wait = 0;                     // diagnostic: cycles spent waiting on the other wave
@@ -306,7 +288,78 @@ __global__ __launch_bounds__(128) void chain_sparse_spec(ChainLaunch L, KParams 
         //   A: each row's tag lookups and tag writes;
         //   B: wait until the chain is done with the slots being reused;
         //   C: write the rows' slots (entries, correction entries, label, step), publish.
+        // Binary-search staging (BS): B, then C with every row's entries, then each row's
+        // correction entries searched in the SK rows before it (slots written above or by
+        // earlier groups; one wave's LDS operations execute in program order).
+        auto stage_group_bs = [&](const Batch& bt, int64_t g, int i0, const Group& G) __attribute__((always_inline)) -> bool {
+            const int64_t u0 = g + i0;
+            const int nq = (int)(n - u0 < 8 ? n - u0 : 8);
+            const int64_t need = u0 + nq - 1 - SR + SK + 1;
+            if ((int64_t)done < need) {
+                if (!spin(&hdr->done, need, 16)) return false;
+                done = __hip_atomic_load(&hdr->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                if (q < nq) {
+                    const int64_t u = u0 + q;
+                    SpecSlot& sl = slots[u % SR];
+                    sl.col[lane] = G.ca[q];
+                    sl.col[lane + 64] = G.cb[q];
+                    sl.val[lane] = G.xa[q];
+                    sl.val[lane + 64] = G.xb[q];
+                    if (lane == 0) {
+                        sl.nnz = (int)(G.e[q] - G.b[q]);
+                        sl.y = readlane_d(bt.y, i0 + q);
+                        sl.s = readlane_d(bt.s, i0 + q);
+                    }
+                }
+            }
+            // (a runtime loop over the group's rows: keys and window rows are read from LDS)
+#pragma unroll 1
+            for (int q = 0; q < nq; ++q) {
+                const int64_t u = u0 + q;
+                SpecSlot& sl = slots[u % SR];
+                const int nnz = sl.nnz;
+                const int32_t ka = sl.col[lane], kb = sl.col[lane + 64];
+                // lower_bound of ka / kb in each window row (oldest first: the newest hit wins)
+                int pos_a[SK], pos_b[SK], m[SK];
+#pragma unroll
+                for (int r = 0; r < SK; ++r) {
+                    pos_a[r] = 0;
+                    pos_b[r] = 0;
+                    m[r] = u - (SK - r) >= 0 ? slots[(u - (SK - r)) % SR].nnz : 0;
+                }
+#pragma unroll 1
+                for (int step = 64; step >= 1; step >>= 1) {
+#pragma unroll
+                    for (int r = 0; r < SK; ++r) {
+                        const int32_t* cw = slots[(u - (SK - r) + SR) % SR].col;
+                        const int pa = pos_a[r] + step - 1, pb = pos_b[r] + step - 1;
+                        const int32_t va = cw[pa], vb = cw[pb];
+                        pos_a[r] += (pa < m[r] && va < ka) ? step : 0;
+                        pos_b[r] += (pb < m[r] && vb < kb) ? step : 0;
+                    }
+                }
+                int32_t pa = -1, pb = -1;
+#pragma unroll
+                for (int r = 0; r < SK; ++r) {
+                    const int32_t* cw = slots[(u - (SK - r) + SR) % SR].col;
+                    const int32_t va = cw[pos_a[r]], vb = cw[pos_b[r]];
+                    const int32_t tag = (SK - r) << 8;
+                    if (pos_a[r] < m[r] && va == ka) pa = tag | pos_a[r];
+                    if (pos_b[r] < m[r] && vb == kb) pb = tag | pos_b[r];
+                }
+                sl.prev[lane] = (int16_t)(lane < nnz ? pa : -1);
+                sl.prev[lane + 64] = (int16_t)(lane + 64 < nnz ? pb : -1);
+            }
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            if (nq > 0)
+                __hip_atomic_store(&hdr->ready, (unsigned)(u0 + nq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return true;
+        };
         auto stage_group = [&](const Batch& bt, int64_t g, int i0, const Group& G) __attribute__((always_inline)) -> bool {
+            if constexpr (BS) return stage_group_bs(bt, g, i0, G);
             const int64_t u0 = g + i0;
             int nq = (int)(n - u0 < 8 ? n - u0 : 8);
             // D
@@ -409,6 +462,7 @@ __global__ __launch_bounds__(128) void chain_sparse_spec(ChainLaunch L, KParams 
 
     // ---------------- chain ----------------
     double alpha = 1.0;
+    double dnsq = 0.0;                        // SquaredL2: ||v||^2 - ||v_0||^2 (this lane)
     double loss_sum = 0.0;
     float loss_blk = 0.0f;
     int64_t count = 0;
@@ -472,6 +526,7 @@ __global__ __launch_bounds__(128) void chain_sparse_spec(ChainLaunch L, KParams 
         const float cv = L2 ? float(double(c) / alpha) : c;
         const float nv0 = __builtin_fmaf(cv, x0, w0);
         const float nv1 = __builtin_fmaf(cv, x1, w1);
+        if constexpr (L2) dnsq += nsq_delta(w0, nv0) + nsq_delta(w1, nv1);
         SpecSlot& slw = slots[t % SR];
         slw.nv[lane] = nv0;
         slw.nv[lane + 64] = nv1;
@@ -498,31 +553,12 @@ __global__ __launch_bounds__(128) void chain_sparse_spec(ChainLaunch L, KParams 
     }
     loss_sum += double(loss_blk);
     if constexpr (GRAD == G_LEAST_SQUARES) loss_sum = loss_sum / 2.0;
-    double nsq = 0.0;
-    double* wo = L.w_out + (int64_t)chain * d;
-    for (int i = lane; i < d; i += 64) {
-        const double wv = alpha * double(__hip_atomic_load(&V[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        wo[i] = wv;
-        if constexpr (L2) nsq += wv * wv;
-    }
-    double rv = 0.0;
-    if constexpr (L2) {
-        nsq = wave_sum(nsq);
-        if (count > 0) {
-            const double nrm = sqrt(nsq);
-            rv = 0.5 * kp.reg * nrm * nrm;
-        }
-    }
-    if (lane == 0) {
-        L.rv[chain] = rv;
-        L.loss[chain] = loss_sum;
-        L.cnt[chain] = count;
-        L.cnt_d[chain] = double(count);
-    }
+    sparse_chain_out<L2>(L, kp, chain, lane, alpha, dnsq, loss_sum, count);
 }
 
-size_t sparse_spec_lds_bytes(int d) {
-    return sizeof(SpecHeader) + SR * sizeof(SpecSlot) + (((size_t)d * 2 + 15) / 16) * 16;
+template <int SK, int SR, bool BS>
+size_t spec_lds_bytes(int d) {
+    return sizeof(SpecHeader) + SR * sizeof(SpecSlot) + (BS ? 0 : (((size_t)d * 2 + 15) / 16) * 16);
 }
 
 bool sparse_path_applies(int layout, int compute, int updater, bool check_conv) {
@@ -549,45 +585,127 @@ static int sparse_grad(const ChainLaunch& L, const KParams& kp, int grad, int up
     }
 }
 
-template <typename S, int GRAD>
-static int spec_upd(const ChainLaunch& L, const KParams& kp, int upd, size_t lds, hipStream_t st) {
-    auto k = upd == U_SIMPLE ? chain_sparse_spec<S, GRAD, U_SIMPLE> : chain_sparse_spec<S, GRAD, U_SQUARED_L2>;
+template <typename S, int GRAD, int SK, int SR, bool BS>
+static int spec_upd(const ChainLaunch& L, const KParams& kp, int upd, hipStream_t st) {
+    const size_t lds = spec_lds_bytes<SK, SR, BS>(kp.d);
+    auto k = upd == U_SIMPLE ? chain_sparse_spec<S, GRAD, U_SIMPLE, SK, SR, BS>
+                             : chain_sparse_spec<S, GRAD, U_SQUARED_L2, SK, SR, BS>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(128), lds, st, L, kp);
     return (int)hipGetLastError();
 }
 
-template <typename S>
-static int spec_grad(const ChainLaunch& L, const KParams& kp, int grad, int upd, size_t lds, hipStream_t st) {
+template <typename S, int SK, int SR, bool BS>
+static int spec_grad(const ChainLaunch& L, const KParams& kp, int grad, int upd, hipStream_t st) {
     switch (grad) {
-    case G_LOGISTIC: return spec_upd<S, G_LOGISTIC>(L, kp, upd, lds, st);
-    case G_LEAST_SQUARES: return spec_upd<S, G_LEAST_SQUARES>(L, kp, upd, lds, st);
-    case G_HINGE: return spec_upd<S, G_HINGE>(L, kp, upd, lds, st);
+    case G_LOGISTIC: return spec_upd<S, G_LOGISTIC, SK, SR, BS>(L, kp, upd, st);
+    case G_LEAST_SQUARES: return spec_upd<S, G_LEAST_SQUARES, SK, SR, BS>(L, kp, upd, st);
+    case G_HINGE: return spec_upd<S, G_HINGE, SK, SR, BS>(L, kp, upd, st);
     default: return -3;
     }
+}
+
+template <int SK, int SR, bool BS>
+static int spec_launch(const ChainLaunch& L, const KParams& kp, int storage, int grad, int upd, hipStream_t st) {
+    if (storage == 1) return spec_grad<float, SK, SR, BS>(L, kp, grad, upd, st);
+    return spec_grad<double, SK, SR, BS>(L, kp, grad, upd, st);
+}
+
+// ------------------------------------------------------------------------------------------
+// Epoch set-up of the fp32 CSR chains: every chain's fp32 weights = float(w_in), written by the
+// whole GPU (a slice of w_in is read once per block and stored to a range of chains), instead of
+// by each chain's one wave before its first sample (2^22 features x 1024 chains = 17 GB);
+// wnsq0 = ||float(w_in)||^2 in f64 (SquaredL2; one block, fixed tree: deterministic).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void wf32_init_kernel(float* __restrict__ wf, int64_t wstride,
+                                                        const double* __restrict__ w_in, int d,
+                                                        int n_chains, int chains_per_block) {
+    const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (i >= d) return;
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = i + k < d ? float(w_in[i + k]) : 0.0f;
+    const int p0 = blockIdx.y * chains_per_block;
+    const int p1 = p0 + chains_per_block < n_chains ? p0 + chains_per_block : n_chains;
+    const bool full = i + 4 <= d;
+    for (int p = p0; p < p1; ++p) {
+        float* dst = wf + (int64_t)p * wstride + i;
+        if (full) {
+            *reinterpret_cast<f32x4*>(dst) = f32x4{v[0], v[1], v[2], v[3]};
+        } else {
+            for (int k = 0; k < 4 && i + k < d; ++k) dst[k] = v[k];
+        }
+    }
+}
+
+__global__ __launch_bounds__(1024) void wnsq0_kernel(const double* __restrict__ w_in, int d,
+                                                     double* __restrict__ out) {
+    __shared__ double s[1024];
+    double t = 0.0;
+    for (int i = threadIdx.x; i < d; i += 1024) {
+        const double v = double(float(w_in[i]));
+        t += v * v;
+    }
+    s[threadIdx.x] = t;
+    __syncthreads();
+    for (int h = 512; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) s[threadIdx.x] += s[threadIdx.x + h];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *out = s[0];
+}
+
+static int sparse_epoch_init(const ChainLaunch& L, const KParams& kp, int updater, hipStream_t st) {
+    const int bx = (kp.d + 1023) / 1024;
+    int by = (2048 + bx - 1) / bx;          // >= 2048 blocks in all
+    by = by < kp.n_chains ? by : kp.n_chains;
+    const int per = (kp.n_chains + by - 1) / by;
+    by = (kp.n_chains + per - 1) / per;
+    hipLaunchKernelGGL(wf32_init_kernel, dim3(bx, by), dim3(256), 0, st, L.wf32, L.wstride, L.w_in,
+                       kp.d, kp.n_chains, per);
+    if (updater == U_SQUARED_L2)
+        hipLaunchKernelGGL(wnsq0_kernel, dim3(1), dim3(1024), 0, st, L.w_in, kp.d, L.wnsq0);
+    return (int)hipGetLastError();
+}
+
+// Speculation depth of the binary-search kernel: 8 rows by default; PSGD_SPARSE_SK = 4 | 16
+// for A/B measurements (read at every launch).
+static int spec_depth() {
+    const char* e = getenv("PSGD_SPARSE_SK");
+    const int v = e ? atoi(e) : 8;
+    return v == 4 || v == 16 ? v : 8;
 }
 
 int launch_sparse_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
                          int updater, int64_t max_nnz, hipStream_t stream, int* kernel_variant) {
     if (kp.n_chains <= 0) return 0;
-    if (!L.wf32 || L.wstride < (int64_t)kp.d + 128) return (int)hipErrorInvalidValue;
-    // PSGD_SPARSE_KERNEL = lds | spec | plain forces a variant (tests, A/B measurements; read
-    // at every launch); default: the first that applies in that order
+    if (!L.wf32 || L.wstride < (int64_t)kp.d + 128 + 1024 || (L.wstride & 3) || !L.walpha || !L.wnsq0)
+        return (int)hipErrorInvalidValue;
+    int rc = sparse_epoch_init(L, kp, updater, stream);
+    if (rc) return rc;
+    // PSGD_SPARSE_KERNEL = lds | spec | bsearch | plain forces a variant (tests, A/B
+    // measurements; read at every launch); default: the first that applies in that order
     const char* force = getenv("PSGD_SPARSE_KERNEL");
     const bool any = !force || !*force;
     const bool no_lds = !any && strcmp(force, "lds") != 0;
     const bool no_spec = !any && strcmp(force, "spec") != 0;
+    const bool no_bs = !any && strcmp(force, "bsearch") != 0;
     // first choice: the chain's weights in LDS (psgd_sparse_lds.hip), for rows of <= 128
     // non-zeros and d up to ~65k features
     if (!no_lds) {
-        const int rc = launch_sparse_lds_chains(L, kp, storage, gradient, updater, max_nnz, stream, kernel_variant);
+        rc = launch_sparse_lds_chains(L, kp, storage, gradient, updater, max_nnz, stream, kernel_variant);
         if (rc != -3) return rc;
     }
-    const size_t lds = sparse_spec_lds_bytes(kp.d);
-    if (!no_spec && max_nnz <= SCAP && lds <= 160 * 1024) {
+    if (!no_spec && max_nnz <= SCAP && spec_lds_bytes<8, 32, false>(kp.d) <= 160 * 1024) {
         if (kernel_variant) *kernel_variant = 410 + storage;
-        if (storage == 1) return spec_grad<float>(L, kp, gradient, updater, lds, stream);
-        return spec_grad<double>(L, kp, gradient, updater, lds, stream);
+        return spec_launch<8, 32, false>(L, kp, storage, gradient, updater, stream);
+    }
+    if (!no_bs && max_nnz <= SCAP) {
+        const int sk = spec_depth();
+        if (kernel_variant) *kernel_variant = 420 + 10 * (sk == 4 ? 1 : sk == 16 ? 2 : 0) + storage;
+        if (sk == 4) return spec_launch<4, 16, true>(L, kp, storage, gradient, updater, stream);
+        if (sk == 16) return spec_launch<16, 64, true>(L, kp, storage, gradient, updater, stream);
+        return spec_launch<8, 32, true>(L, kp, storage, gradient, updater, stream);
     }
     if (kernel_variant) *kernel_variant = 400 + storage;
     if (storage == 1) return sparse_grad<float>(L, kp, gradient, updater, stream);

@@ -156,10 +156,7 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
     for (int64_t i = threadIdx.x; i < T; i += blockDim.x) tagpos[i] = 0xFFFF;
     for (int i = threadIdx.x; i < K; i += blockDim.x) W[i] = float(as_global(L.w_in)[i]);
     if (threadIdx.x < 8) reinterpret_cast<unsigned*>(hdr)[threadIdx.x] = 0;
-    if (wave == 0) {
-        // the chain's tail gathers below are loads of these addresses from the same wave
-        for (int i = K + lane; i < d; i += 64) as_global_mut(V)[i] = float(as_global(L.w_in)[i]);
-    }
+    // the tail V[K, d) starts as float(w_in) (wf32_init_kernel, launched before this kernel)
     __syncthreads();
 
     uint64_t st_wait = 0;                     // diagnostic (PSGD_STAMPS): cycles spent waiting
@@ -398,6 +395,7 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
     // have a consumer: the compiler treats an asm load's result as written at issue, and a dead
     // one's registers could be reused while the load is still in flight.
     double alpha = 1.0;       // SquaredL2: w = alpha * v
+    double dnsq = 0.0;        // SquaredL2: ||v||^2 - ||v_0||^2 (this lane)
     double loss_sum = 0.0;
     float loss_blk = 0.0f;
     int64_t count = 0;
@@ -508,6 +506,7 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
         const float cv = L2 ? float(double(c) / alpha) : c;
         const float nv0 = __builtin_fmaf(cv, cur.x0, w0);
         const float nv1 = __builtin_fmaf(cv, cur.x1, w1);
+        if constexpr (L2) dnsq += nsq_delta(w0, nv0) + nsq_delta(w1, nv1);
         lds[cur.rw0 >> 16] = nv0;
         lds[cur.rw1 >> 16] = nv1;
         // this row's tail stores (2 VMEM instructions)
@@ -530,29 +529,10 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
     stamp_out(0);
     loss_sum += double(loss_blk);
     if constexpr (GRAD == G_LEAST_SQUARES) loss_sum = loss_sum / 2.0;
-    // the chain's weights (w = alpha v) and regVal of its last update (PSGD.scala:257)
-    double nsq = 0.0;
-    double* wo = L.w_out + (int64_t)chain * d;
-    for (int i = lane; i < d; i += 64) {
-        const float v = i < K ? W[i] : __hip_atomic_load(&V[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const double wv = alpha * double(v);
-        wo[i] = wv;
-        if constexpr (L2) nsq += wv * wv;
-    }
-    double rv = 0.0;
-    if constexpr (L2) {
-        nsq = wave_sum(nsq);
-        if (count > 0) {
-            const double nrm = sqrt(nsq);
-            rv = 0.5 * kp.reg * nrm * nrm;
-        }
-    }
-    if (lane == 0) {
-        L.rv[chain] = rv;
-        L.loss[chain] = loss_sum;
-        L.cnt[chain] = count;
-        L.cnt_d[chain] = double(count);
-    }
+    // the LDS head joins the tail in L.wf32 (the fold reads w = alpha v from there); regVal
+    // of the chain's last update (PSGD.scala:257) from the tracked ||v||^2
+    for (int i = lane; i < K; i += 64) V[i] = W[i];
+    sparse_chain_out<L2>(L, kp, chain, lane, alpha, dnsq, loss_sum, count);
 }
 
 template <typename S, int GRAD, int SK>

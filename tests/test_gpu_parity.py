@@ -144,6 +144,37 @@ def test_dense_stateful_updaters(pkg, oracle, upd):
         assert_close(h, hr, what=f"{upd} tol={tol} loss")
 
 
+@pytest.mark.parametrize("upd", ["adagrad", "adam", "l1"])
+@pytest.mark.parametrize("d,dtype", [(40, np.float64), (512, np.float32), (1024, np.float64), (2048, np.float32)])
+def test_dense_fp32_throughput_updaters(pkg, oracle, upd, d, dtype):
+    """AdaGrad / Adam / L1 in the fp32 throughput mode: chain_dense with the updater status in
+    registers (variant 10x), against the fp64 oracle at the fp32 tolerance, tol 0
+    and tol > 0 (per-sample breaks: counts may differ only when tol > 0)."""
+    rng = np.random.default_rng(d + len(upd))
+    n, P = 8000, 4
+    X, y = synth(rng, n, d, "logistic", dtype)
+    data = pkg.PartitionedData.parallelize(y, X, P, dtype=dtype)
+    offs = [i * n // P for i in range(P)] + [n]
+    step = 0.01
+    reg = 0.001 if upd == "l1" else 0.0
+    for tol in (0.0, 0.001):
+        w, h = pkg.runParallelizedSGD(data, pkg.LogisticGradient(), getattr(pkg, U[upd])(), step, 3, reg, 1.0,
+                                      np.zeros(d), tol, compute_dtype="f32")
+        es = np.dtype(dtype).itemsize
+        nv = 1
+        while nv * 64 * 16 // es < d:
+            nv *= 2
+        assert pkg.optimization.get_context(0).last_kernel() == 100 + nv
+        wr, hr, _ = oracle.run(oracle.Matrix(y, X.astype(np.float64)), offs, "logistic", upd, step, 3, reg,
+                               np.zeros(d), tol=tol, n_threads=8)
+        if tol > 0 and len(h) != len(hr):
+            continue   # a break on the other side of the fp32/fp64 rounding (allowed when tol > 0)
+        scale = np.max(np.abs(wr))
+        err = np.max(np.abs(w - wr)) / scale
+        assert err <= FP32_REL, f"{upd} d={d} tol={tol}: weights {err:.3g} x max|w|"
+        assert_close(h, hr, rel=FP32_LOSS_REL, what=f"{upd} d={d} tol={tol} fp32 loss")
+
+
 def test_kernel_selection(pkg, oracle):
     """fp64 compute: tol = 0 with Simple/SquaredL2 runs the blocked fp64 kernel (50x), tol > 0
     the per-sample chain_dense (10x), d past the register-resident range chain_general (200)."""
