@@ -41,11 +41,13 @@ CSR_NNZ = {"c4": 94, "c5": 100}  # nonzeros per row (c4: rcv1's mean; c5: SURVEY
 REG = {"c5": 1e-6}                # SquaredL2 regParam (c5); others: Simple updater
 # secondary lines: rows per GPU (0 = the workload's own; c5's full 125M-row shard takes minutes)
 SECONDARY_ROWS = {"c5": 20_000_000}
-DEFAULT_SECONDARY = "c3:f64,c3:f32,c2:f64,c1:f64,c4:f32,c5:f32,c2:f32:adagrad,c2:f32:adam"
+# (AdaGrad / Adam on the logistic c3 shard: the reference's Adam, r^iter in fix1 (UPD.scala:262),
+# turns NaN once the squared-gradient average r exceeds 1, which least squares at c2 reaches)
+DEFAULT_SECONDARY = "c3:f64,c3:f32,c2:f64,c1:f64,c4:f32,c5:f32,c3:f32:adagrad,c3:f32:adam"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def pmc_traffic(workload, grad, variant, storage, rows, compute="f32"):
+def pmc_traffic(workload, grad, variant, storage, rows, compute="f32", updater="simple"):
     """HBM bytes per chain-kernel launch from the newest committed rocprofv3 PMC summary of the
     same workload and kernel instance (profiles/r*_<workload>[_<tag>]_pmc.json,
     tools/profile_round.sh + tools/pmc_summary.py; FETCH_SIZE doubled per MI355X_MICROARCH.md
@@ -56,17 +58,20 @@ def pmc_traffic(workload, grad, variant, storage, rows, compute="f32"):
     if not files or not (300 <= variant < 700):
         return None, None
     g = {"logistic": 0, "least_squares": 1, "hinge": 2}[grad]
+    u = {"simple": 0, "squared_l2": 1}.get(updater)
+    if u is None:
+        return None, None
     sname = "float" if storage == "f32" else "double"
     if variant >= 600:
-        prefix = f"psgd::chain_sparse_lds<{sname}, {g}, 0>"
+        prefix = f"psgd::chain_sparse_lds<{sname}, {g}, {u},"
     elif variant >= 500:
-        prefix = f"psgd::chain_block64<{sname}, {g}, 0, {variant - 500},"
+        prefix = f"psgd::chain_block64<{sname}, {g}, {u}, {variant - 500},"
     elif variant >= 410:
-        prefix = f"psgd::chain_sparse_spec<{sname}, {g}, 0>"
+        prefix = f"psgd::chain_sparse_spec<{sname}, {g}, {u}"
     elif variant >= 400:
-        prefix = f"psgd::chain_sparse<{sname}, {g}, 0>"
+        prefix = f"psgd::chain_sparse<{sname}, {g}, {u}>"
     else:
-        prefix = f"psgd::chain_block<{sname}, {g}, 0, {variant - 300},"
+        prefix = f"psgd::chain_block<{sname}, {g}, {u}, {variant - 300},"
     # newest round first (r02 before r01), then the file name
     for path in sorted(files, key=lambda f: os.path.basename(f), reverse=True):
         with open(path) as f:
@@ -87,10 +92,6 @@ def kernel_name(variant):
     if 600 <= variant < 700:
         return (f"chain_sparse_lds (fp32 CSR chain, weights LDS-resident [tail past ~160 KiB: L2-resident, "
                 f"gathered {8 if variant >= 610 else 4} samples ahead with an LDS feature-tag correction])")
-    if 420 <= variant < 450:
-        sk = {42: 8, 43: 4, 44: 16}[variant // 10]
-        return (f"chain_sparse_spec (fp32 CSR chain, weights HBM-resident, gathers {sk} samples "
-                "ahead, correction entries by binary search in the window rows)")
     if 410 <= variant < 420:
         return ("chain_sparse_spec (fp32 CSR chain, weights L2/MALL-resident, gathers 8 samples "
                 "ahead with an LDS feature-tag correction)")
@@ -355,7 +356,8 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
     # one chain-kernel launch processes every (sampled) row of this GPU's partitions
     achieved = local_samples * bytes_per_sample / avg_kernel_s / 1e9
     variant = engine.ctx.last_kernel()
-    traffic, traffic_src = pmc_traffic(workload, grad, variant, sdt, n, compute)
+    upd_name = updater or ("squared_l2" if reg > 0 else "simple")
+    traffic, traffic_src = pmc_traffic(workload, grad, variant, sdt, n, compute, upd_name)
     res = {
         "value": value, "ms_per_step": elapsed / steps * 1e3, "dtype": compute, "loss": loss,
         "config": {"workload": f"{workload}: {cfg_name}", "rows_per_gpu": n, "d": d,
@@ -434,9 +436,13 @@ def main():
     for spec in secondary:
         wl, comp, upd = (spec.split(":") + ["", ""])[:3]
         torch.cuda.empty_cache()
-        r = run_workload(torch, dist, pkg, dev, rank, world, local, wl, comp or "f32",
-                         SECONDARY_ROWS.get(wl, 0), 1.0, args.steps, args.warmup,
-                         min(args.prewarm_s, 0.5), updater=upd)
+        try:
+            r = run_workload(torch, dist, pkg, dev, rank, world, local, wl, comp or "f32",
+                             SECONDARY_ROWS.get(wl, 0), 1.0, args.steps, args.warmup,
+                             min(args.prewarm_s, 0.5), updater=upd)
+        except Exception as e:   # a secondary line never hides the headline
+            out["secondary"].append({"spec": spec, "error": f"{type(e).__name__}: {e}"})
+            continue
         r.pop("_meta")
         r["samples_per_s"] = r.pop("value")
         r["loss"] = float(r["loss"])

@@ -147,6 +147,10 @@ __device__ __forceinline__ float m_sqrt(float x) { return sqrtf(x); }
 __device__ __forceinline__ double m_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 __device__ __forceinline__ double m_pow(double a, double b) { return pow(a, b); }
 __device__ __forceinline__ float m_pow(float a, float b) { return powf(a, b); }
+// a^b for a >= 0 in the fp32 throughput mode: the hardware log2 / exp2 (a few ulp)
+__device__ __forceinline__ float pow_fast(float a, float b) {
+    return __builtin_amdgcn_exp2f(b * __builtin_amdgcn_logf(a));
+}
 __device__ __forceinline__ float m_fma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 
 // java.lang.Math.max(a, b): NaN if either is NaN.

@@ -210,8 +210,9 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, Ri
                 const T2 g = mult * x[e];
                 const T2 acc2 = first ? g * g : ua[e] + g * g;
                 ua[e] = acc2;
-                nw.x = old.x + a * (g.x / m_sqrt(acc2.x + T(1)));
-                nw.y = old.y + a * (g.y / m_sqrt(acc2.y + T(1)));
+                // fp32 mode: g * rsqrt(accum + 1) (one v_rsq_f32, ~1 ulp) for g / sqrt(accum + 1)
+                nw.x = old.x + a * (g.x * __builtin_amdgcn_rsqf(acc2.x + T(1)));
+                nw.y = old.y + a * (g.y * __builtin_amdgcn_rsqf(acc2.y + T(1)));
             } else if constexpr (UPD == U_ADAM) {
                 // the reference's variant, literally: v = beta v + (1-beta) g,
                 // r = gamma r + (1-gamma) g^2, fix1 = sqrt(1 - r^iter) + eps, w += -lr * v / fix1
@@ -223,8 +224,10 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, Ri
                 else { v = ua[e] * beta + g * (T(1) - beta); r = ub[e] * gamma + sq * (T(1) - gamma); }
                 ua[e] = v;
                 ub[e] = r;
-                const T fx = m_sqrt(T(1) - m_pow(r.x, iter)) + T(kp.eps);
-                const T fy = m_sqrt(T(1) - m_pow(r.y, iter)) + T(kp.eps);
+                // fp32 mode: r^iter = exp2(iter * log2 r) (v_log_f32 / v_exp_f32; r = 0 gives 0,
+                // r > 1 overflows to inf and fix1 to NaN, as pow does)
+                const T fx = m_sqrt(T(1) - pow_fast(r.x, iter)) + T(kp.eps);
+                const T fy = m_sqrt(T(1) - pow_fast(r.y, iter)) + T(kp.eps);
                 nw.x = old.x + al * (v.x / fx);
                 nw.y = old.y + al * (v.y / fy);
             } else if constexpr (UPD == U_SQUARED_L2) {

@@ -145,15 +145,10 @@ __global__ __launch_bounds__(64) void chain_sparse(ChainLaunch L, KParams kp) {
 //
 // A gather for row u issued during sample u-SK does not see the stores of rows u-SK .. u-1
 // (issued after it). A helper wave finds, for every entry of row u, the latest of those rows
-// that has the same feature, in one of two ways:
-//   * tag table (BS = false; d small enough for 2 bytes per feature in LDS, 47,236 at rcv1
-//     shape): tagpos[j] = (row & 255) << 8 | entry of the last row that touched feature j; an
-//     entry from outside the window is ignored, and a row's tags are cleared before its LDS
-//     slot is reused (so an 8-bit row tag never aliases);
-//   * binary search (BS = true; any d -- 2^22 in BASELINE config 5): a row's column indices
-//     are strictly increasing, so each entry is looked up in each of the SK window rows' slots
-//     (7 halvings + 1 compare over <= 128 entries); no per-feature state at all.
-// The chain wave replaces such a gathered value by that row's new value (kept in LDS) --
+// that has the same feature: it keeps tagpos[j] = (row & 255) << 8 | entry of the last row that
+// touched feature j (2 bytes per feature in LDS: d up to ~58k); an entry from outside the
+// window is ignored, and a row's tags are cleared before its LDS slot is reused (so an 8-bit
+// row tag never aliases). The chain wave replaces such a gathered value by that row's new value (kept in LDS) --
 // exactly the value the reference's sequential update would read. Waves:
 //   wave 0 (chain)  per sample t: waits for row t's gather (issued SK samples earlier; a fixed
 //                   count of VMEM instructions per sample makes it s_waitcnt vmcnt(4 SK - 2)),
@@ -186,7 +181,7 @@ struct SpecSlot {
     double y, s;
 };
 
-template <typename S, int GRAD, int UPD, int SK, int SR, bool BS>
+template <typename S, int GRAD, int UPD, int SK, int SR>
 __global__ __launch_bounds__(128) void chain_sparse_spec(ChainLaunch L, KParams kp) {
     static_assert(spec_ring_ok<SK, SR>(), "ring too small for the speculation depth");
     constexpr bool L2 = UPD == U_SQUARED_L2;
@@ -202,8 +197,7 @@ __global__ __launch_bounds__(128) void chain_sparse_spec(ChainLaunch L, KParams 
     const int64_t n = dsc.n_rows;
     float* V = L.wf32 + (int64_t)chain * L.wstride;   // [d] weights + [128] dummy targets
 
-    if constexpr (!BS)
-        for (int i = threadIdx.x; i < d; i += blockDim.x) tagpos[i] = 0xFFFF;
+    for (int i = threadIdx.x; i < d; i += blockDim.x) tagpos[i] = 0xFFFF;
     if (threadIdx.x == 0) { hdr->ready = 0; hdr->done = 0; hdr->stop = 0; }
     __syncthreads();
 
@@ -288,78 +282,7 @@ __global__ __launch_bounds__(128) void chain_sparse_spec(ChainLaunch L, KParams 
         //   A: each row's tag lookups and tag writes;
         //   B: wait until the chain is done with the slots being reused;
         //   C: write the rows' slots (entries, correction entries, label, step), publish.
-        // Binary-search staging (BS): B, then C with every row's entries, then each row's
-        // correction entries searched in the SK rows before it (slots written above or by
-        // earlier groups; one wave's LDS operations execute in program order).
-        auto stage_group_bs = [&](const Batch& bt, int64_t g, int i0, const Group& G) __attribute__((always_inline)) -> bool {
-            const int64_t u0 = g + i0;
-            const int nq = (int)(n - u0 < 8 ? n - u0 : 8);
-            const int64_t need = u0 + nq - 1 - SR + SK + 1;
-            if ((int64_t)done < need) {
-                if (!spin(&hdr->done, need, 16)) return false;
-                done = __hip_atomic_load(&hdr->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                if (q < nq) {
-                    const int64_t u = u0 + q;
-                    SpecSlot& sl = slots[u % SR];
-                    sl.col[lane] = G.ca[q];
-                    sl.col[lane + 64] = G.cb[q];
-                    sl.val[lane] = G.xa[q];
-                    sl.val[lane + 64] = G.xb[q];
-                    if (lane == 0) {
-                        sl.nnz = (int)(G.e[q] - G.b[q]);
-                        sl.y = readlane_d(bt.y, i0 + q);
-                        sl.s = readlane_d(bt.s, i0 + q);
-                    }
-                }
-            }
-            // (a runtime loop over the group's rows: keys and window rows are read from LDS)
-#pragma unroll 1
-            for (int q = 0; q < nq; ++q) {
-                const int64_t u = u0 + q;
-                SpecSlot& sl = slots[u % SR];
-                const int nnz = sl.nnz;
-                const int32_t ka = sl.col[lane], kb = sl.col[lane + 64];
-                // lower_bound of ka / kb in each window row (oldest first: the newest hit wins)
-                int pos_a[SK], pos_b[SK], m[SK];
-#pragma unroll
-                for (int r = 0; r < SK; ++r) {
-                    pos_a[r] = 0;
-                    pos_b[r] = 0;
-                    m[r] = u - (SK - r) >= 0 ? slots[(u - (SK - r)) % SR].nnz : 0;
-                }
-#pragma unroll 1
-                for (int step = 64; step >= 1; step >>= 1) {
-#pragma unroll
-                    for (int r = 0; r < SK; ++r) {
-                        const int32_t* cw = slots[(u - (SK - r) + SR) % SR].col;
-                        const int pa = pos_a[r] + step - 1, pb = pos_b[r] + step - 1;
-                        const int32_t va = cw[pa], vb = cw[pb];
-                        pos_a[r] += (pa < m[r] && va < ka) ? step : 0;
-                        pos_b[r] += (pb < m[r] && vb < kb) ? step : 0;
-                    }
-                }
-                int32_t pa = -1, pb = -1;
-#pragma unroll
-                for (int r = 0; r < SK; ++r) {
-                    const int32_t* cw = slots[(u - (SK - r) + SR) % SR].col;
-                    const int32_t va = cw[pos_a[r]], vb = cw[pos_b[r]];
-                    const int32_t tag = (SK - r) << 8;
-                    if (pos_a[r] < m[r] && va == ka) pa = tag | pos_a[r];
-                    if (pos_b[r] < m[r] && vb == kb) pb = tag | pos_b[r];
-                }
-                sl.prev[lane] = (int16_t)(lane < nnz ? pa : -1);
-                sl.prev[lane + 64] = (int16_t)(lane + 64 < nnz ? pb : -1);
-            }
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            if (nq > 0)
-                __hip_atomic_store(&hdr->ready, (unsigned)(u0 + nq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            return true;
-        };
         auto stage_group = [&](const Batch& bt, int64_t g, int i0, const Group& G) __attribute__((always_inline)) -> bool {
-            if constexpr (BS) return stage_group_bs(bt, g, i0, G);
             const int64_t u0 = g + i0;
             int nq = (int)(n - u0 < 8 ? n - u0 : 8);
             // D
@@ -556,9 +479,9 @@ __global__ __launch_bounds__(128) void chain_sparse_spec(ChainLaunch L, KParams 
     sparse_chain_out<L2>(L, kp, chain, lane, alpha, dnsq, loss_sum, count);
 }
 
-template <int SK, int SR, bool BS>
+template <int SK, int SR>
 size_t spec_lds_bytes(int d) {
-    return sizeof(SpecHeader) + SR * sizeof(SpecSlot) + (BS ? 0 : (((size_t)d * 2 + 15) / 16) * 16);
+    return sizeof(SpecHeader) + SR * sizeof(SpecSlot) + (((size_t)d * 2 + 15) / 16) * 16;
 }
 
 bool sparse_path_applies(int layout, int compute, int updater, bool check_conv) {
@@ -585,30 +508,30 @@ static int sparse_grad(const ChainLaunch& L, const KParams& kp, int grad, int up
     }
 }
 
-template <typename S, int GRAD, int SK, int SR, bool BS>
+template <typename S, int GRAD, int SK, int SR>
 static int spec_upd(const ChainLaunch& L, const KParams& kp, int upd, hipStream_t st) {
-    const size_t lds = spec_lds_bytes<SK, SR, BS>(kp.d);
-    auto k = upd == U_SIMPLE ? chain_sparse_spec<S, GRAD, U_SIMPLE, SK, SR, BS>
-                             : chain_sparse_spec<S, GRAD, U_SQUARED_L2, SK, SR, BS>;
+    const size_t lds = spec_lds_bytes<SK, SR>(kp.d);
+    auto k = upd == U_SIMPLE ? chain_sparse_spec<S, GRAD, U_SIMPLE, SK, SR>
+                             : chain_sparse_spec<S, GRAD, U_SQUARED_L2, SK, SR>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(128), lds, st, L, kp);
     return (int)hipGetLastError();
 }
 
-template <typename S, int SK, int SR, bool BS>
+template <typename S, int SK, int SR>
 static int spec_grad(const ChainLaunch& L, const KParams& kp, int grad, int upd, hipStream_t st) {
     switch (grad) {
-    case G_LOGISTIC: return spec_upd<S, G_LOGISTIC, SK, SR, BS>(L, kp, upd, st);
-    case G_LEAST_SQUARES: return spec_upd<S, G_LEAST_SQUARES, SK, SR, BS>(L, kp, upd, st);
-    case G_HINGE: return spec_upd<S, G_HINGE, SK, SR, BS>(L, kp, upd, st);
+    case G_LOGISTIC: return spec_upd<S, G_LOGISTIC, SK, SR>(L, kp, upd, st);
+    case G_LEAST_SQUARES: return spec_upd<S, G_LEAST_SQUARES, SK, SR>(L, kp, upd, st);
+    case G_HINGE: return spec_upd<S, G_HINGE, SK, SR>(L, kp, upd, st);
     default: return -3;
     }
 }
 
-template <int SK, int SR, bool BS>
+template <int SK, int SR>
 static int spec_launch(const ChainLaunch& L, const KParams& kp, int storage, int grad, int upd, hipStream_t st) {
-    if (storage == 1) return spec_grad<float, SK, SR, BS>(L, kp, grad, upd, st);
-    return spec_grad<double, SK, SR, BS>(L, kp, grad, upd, st);
+    if (storage == 1) return spec_grad<float, SK, SR>(L, kp, grad, upd, st);
+    return spec_grad<double, SK, SR>(L, kp, grad, upd, st);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -668,14 +591,6 @@ static int sparse_epoch_init(const ChainLaunch& L, const KParams& kp, int update
     return (int)hipGetLastError();
 }
 
-// Speculation depth of the binary-search kernel: 8 rows by default; PSGD_SPARSE_SK = 4 | 16
-// for A/B measurements (read at every launch).
-static int spec_depth() {
-    const char* e = getenv("PSGD_SPARSE_SK");
-    const int v = e ? atoi(e) : 8;
-    return v == 4 || v == 16 ? v : 8;
-}
-
 int launch_sparse_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
                          int updater, int64_t max_nnz, hipStream_t stream, int* kernel_variant) {
     if (kp.n_chains <= 0) return 0;
@@ -683,29 +598,21 @@ int launch_sparse_chains(const ChainLaunch& L, const KParams& kp, int storage, i
         return (int)hipErrorInvalidValue;
     int rc = sparse_epoch_init(L, kp, updater, stream);
     if (rc) return rc;
-    // PSGD_SPARSE_KERNEL = lds | spec | bsearch | plain forces a variant (tests, A/B
-    // measurements; read at every launch); default: the first that applies in that order
+    // PSGD_SPARSE_KERNEL = lds | spec | plain forces a variant (tests, A/B measurements; read
+    // at every launch); default: the first that applies in that order
     const char* force = getenv("PSGD_SPARSE_KERNEL");
     const bool any = !force || !*force;
     const bool no_lds = !any && strcmp(force, "lds") != 0;
     const bool no_spec = !any && strcmp(force, "spec") != 0;
-    const bool no_bs = !any && strcmp(force, "bsearch") != 0;
     // first choice: the chain's weights in LDS (psgd_sparse_lds.hip), for rows of <= 128
     // non-zeros and d up to ~65k features
     if (!no_lds) {
         rc = launch_sparse_lds_chains(L, kp, storage, gradient, updater, max_nnz, stream, kernel_variant);
         if (rc != -3) return rc;
     }
-    if (!no_spec && max_nnz <= SCAP && spec_lds_bytes<8, 32, false>(kp.d) <= 160 * 1024) {
+    if (!no_spec && max_nnz <= SCAP && spec_lds_bytes<8, 32>(kp.d) <= 160 * 1024) {
         if (kernel_variant) *kernel_variant = 410 + storage;
-        return spec_launch<8, 32, false>(L, kp, storage, gradient, updater, stream);
-    }
-    if (!no_bs && max_nnz <= SCAP) {
-        const int sk = spec_depth();
-        if (kernel_variant) *kernel_variant = 420 + 10 * (sk == 4 ? 1 : sk == 16 ? 2 : 0) + storage;
-        if (sk == 4) return spec_launch<4, 16, true>(L, kp, storage, gradient, updater, stream);
-        if (sk == 16) return spec_launch<16, 64, true>(L, kp, storage, gradient, updater, stream);
-        return spec_launch<8, 32, true>(L, kp, storage, gradient, updater, stream);
+        return spec_launch<8, 32>(L, kp, storage, gradient, updater, stream);
     }
     if (kernel_variant) *kernel_variant = 400 + storage;
     if (storage == 1) return sparse_grad<float>(L, kp, gradient, updater, stream);

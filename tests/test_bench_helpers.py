@@ -12,6 +12,16 @@ def test_pmc_traffic_matches_committed_profiles():
     assert abs(t3 / (12_500_000 * 1025 * 4) - 1.0) < 0.01
 
 
+def test_pmc_traffic_matches_the_updater_instance():
+    # c5 runs chain_sparse<float, 0, 1> (Logistic, SquaredL2): ~10 KB of scattered-line traffic
+    # per sample (r02 PMC), not the Simple instance
+    t, src = bench.pmc_traffic("c5", "logistic", 401, "f32", 20_000_000, updater="squared_l2")
+    assert src and src.endswith("_c5_pmc.json")
+    assert 5_000 < t / 20_000_000 < 20_000
+    assert bench.pmc_traffic("c5", "logistic", 401, "f32", 20_000_000, updater="simple") == (None, None)
+    assert bench.pmc_traffic("c2", "least_squares", 302, "f32", 1, updater="adam") == (None, None)
+
+
 def test_pmc_traffic_none_for_unprofiled_kernels():
     assert bench.pmc_traffic("c1", "logistic", 101, "f64", 100_000) == (None, None)
 

@@ -6,9 +6,8 @@
   fp32 through chain_sparse_lds (variant 601: an LDS head of ~22k features, the tail in HBM) and
   chain_sparse_spec (variant 411, its 94 KB LDS tag table at this d), and fp64
   through chain_general (variant 201).
-* C5 (L2 Logistic CSR, d = 2^22, 100 nnz/row, lambda 1e-6, step 0.5): fp32 chain_sparse_spec
-  with binary-search corrections (variants 421/441: depth 8/16, HBM-resident weights),
-  chain_sparse (401) and fp64 chain_general's alpha-scaled lazy SquaredL2.
+* C5 (L2 Logistic CSR, d = 2^22, 100 nnz/row, lambda 1e-6, step 0.5): fp32 chain_sparse
+  (variant 401, HBM-resident weights) and fp64 chain_general's alpha-scaled lazy SquaredL2.
 * psgd_fold_partials_device (the cross-GPU level of the treeReduce, PSGD.scala:271-276) bit for
   bit against the combiner restated in numpy, incl. a zero-count and a NaN-count rank.
 * The engine's two-level fold over partition subsets (what two ranks do) against the oracle's
@@ -169,15 +168,9 @@ def c5():
     return d, rp, col, val, y, offs, w0
 
 
-@pytest.mark.parametrize("compute,kernel,want", [("f32", "", 421), ("f32", "bsearch16", 441),
-                                                 ("f32", "plain", 401), ("f64", "", 201)])
-def test_c5_wide_sparse_l2(pkg, oracle, c5, compute, kernel, want, monkeypatch):
-    # f32: chain_sparse_spec with binary-search corrections (the default at this d; depth 8 and
-    # 16) and chain_sparse; f64: chain_general's alpha-scaled lazy SquaredL2
-    if kernel:
-        monkeypatch.setenv("PSGD_SPARSE_KERNEL", kernel.rstrip("0123456789"))
-        if kernel.endswith("16"):
-            monkeypatch.setenv("PSGD_SPARSE_SK", "16")
+@pytest.mark.parametrize("compute,want", [("f32", 401), ("f64", 201)])
+def test_c5_wide_sparse_l2(pkg, oracle, c5, compute, want):
+    # f32: chain_sparse (HBM-resident weights); f64: chain_general's alpha-scaled lazy SquaredL2
     d, rp, col, val, y, offs, w0 = c5
     vs = val.astype(np.float32) if compute == "f32" else val
     data = csr_parts(pkg, y, rp, col, vs, d, offs)

@@ -3,13 +3,11 @@ step 1.0, 3 iterations, 256 chains per GPU) against the fp64 oracle on the same 
 rows: SURVEY §8c asks for a stated fp32 tolerance; ParallelizedSGD.scala:283 is the loss history
 it is stated on.
 
-What holds at step 1.0 (measured, tests below assert it):
-* the loss history within FP32_C3_LOSS_REL relative;
-* the averaged weights within FP32_C3_W_REL of max|w| (the fold over 256 chains averages the
-  per-chain differences), element-wise relative error only where |w_i| is not small.
-Per-chain weights are not a parity quantity at this step: with ||x||^2 ~ 1,024 every sample
-moves w by O(1), so a single chain's fp32 and fp64 trajectories separate within a few hundred
-samples (the fp64 parity mode, chain_block64, is the mode to use for per-chain parity).
+Measured, and pinned here per chain length: the standard fp32 tolerance
+(2e-4 x max|w| on the weights, 1e-4 on the loss) holds for 40 and 200 rows per chain and at
+C3's own chain length (48,828 rows, 8 chains), not at 2,000 rows per chain (3.7e-3 / 1.0e-4):
+with ||x||^2 ~ 1,024 every early sample moves w by O(1), so the fp32/fp64 difference depends on
+the trajectory. fp64 (chain_block64) is the parity mode; it is checked here at 1e-9 as well.
 """
 import numpy as np
 import pytest
@@ -18,8 +16,9 @@ from conftest import has_gpu
 
 pytestmark = pytest.mark.gpu
 
-FP32_C3_LOSS_REL = 2e-3
-FP32_C3_W_REL = 2e-2
+# (weights x max|w|, loss relative) per chain length: the standard fp32 tolerance
+# holds for short chains; the fp32/fp64 difference grows with the chain at step 1.0
+FP32_C3_TOL = {40: (2e-4, 1e-4), 200: (2e-4, 1e-4), 2000: (1e-2, 5e-4), 48828: (2e-4, 1e-4)}
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -39,9 +38,9 @@ def c3_prefix(P=256, per=200, d=1024, seed=44):
     return X, y, offs
 
 
-@pytest.mark.parametrize("per", [40, 200])
-def test_fp32_at_c3_hyper_parameters(pkg, oracle, per):
-    X, y, offs = c3_prefix(per=per)
+@pytest.mark.parametrize("P,per", [(256, 40), (256, 200), (64, 2000), (8, 48828)])
+def test_fp32_at_c3_hyper_parameters(pkg, oracle, P, per):
+    X, y, offs = c3_prefix(P=P, per=per)
     d = X.shape[1]
     parts = [pkg.DensePartition(y[a:b], X[a:b]) for a, b in zip(offs[:-1], offs[1:])]
     data = pkg.PartitionedData(parts)
@@ -60,6 +59,7 @@ def test_fp32_at_c3_hyper_parameters(pkg, oracle, per):
     print(f"\nC3 prefix {len(offs) - 1} chains x {per} rows, step 1.0, 3 iterations: fp32 weights "
           f"{err_w:.3g} x max|w| (element-wise {err_w_elem:.3g} where |w| > 0.1 max), loss {err_h:.3g} "
           f"relative; fp64 mode {rel64:.3g}")
+    tol_w, tol_h = FP32_C3_TOL[per]
     assert rel64 < 1e-9
-    assert err_h <= FP32_C3_LOSS_REL, err_h
-    assert err_w <= FP32_C3_W_REL, err_w
+    assert err_h <= tol_h, err_h
+    assert err_w <= tol_w, err_w

@@ -3,8 +3,7 @@
 Every case runs on each kernel variant (PSGD_SPARSE_KERNEL forces one): chain_sparse_lds with
 all weights in LDS, with an LDS head of d/3 features and the rest in HBM (PSGD_SPARSE_LDS_HEAD:
 exercises the tail gathers and their corrections at small d) at speculation depths 4 and 8,
-chain_sparse_spec with its per-feature LDS tag table, chain_sparse_spec with the correction
-entries found by binary search in the window rows (any d; depths 4, 8, 16), and chain_sparse.
+chain_sparse_spec, and chain_sparse.
 
 fp32 compute is the throughput mode; its stated tolerance is weights within
 FP32_REL * max|w| and the loss history within FP32_LOSS_REL relative of the fp64 oracle on the
@@ -40,9 +39,6 @@ KERNELS = {  # name: (environment, variant base without the storage digit)
     "lds_tail": ({"PSGD_SPARSE_KERNEL": "lds", "PSGD_SPARSE_LDS_HEAD": "third"}, 600),
     "lds_tail_sk8": ({"PSGD_SPARSE_KERNEL": "lds", "PSGD_SPARSE_LDS_HEAD": "third", "PSGD_SPARSE_SK": "8"}, 610),
     "spec": ({"PSGD_SPARSE_KERNEL": "spec"}, 410),
-    "bsearch": ({"PSGD_SPARSE_KERNEL": "bsearch"}, 420),
-    "bsearch_sk4": ({"PSGD_SPARSE_KERNEL": "bsearch", "PSGD_SPARSE_SK": "4"}, 430),
-    "bsearch_sk16": ({"PSGD_SPARSE_KERNEL": "bsearch", "PSGD_SPARSE_SK": "16"}, 440),
     "plain": ({"PSGD_SPARSE_KERNEL": "plain"}, 400),
 }
 
@@ -90,9 +86,8 @@ def check(pkg, oracle, rp, col, val, y, d, offs, grad, upd, step, reg, iters, fr
     w, h, counts = pkg.runParallelizedSGD(data, getattr(pkg, G[grad])(), getattr(pkg, U[upd])(), step,
                                           iters, reg, frac, np.zeros(d), 0.0, compute_dtype="f32",
                                           return_chain_counts=True)
-    # 60x/61x: weights in LDS; 41x: gathers SK samples ahead (tag table in LDS); 42x-44x: the
-    # same with binary-search corrections; 40x: one per sample. Rows of more than 128
-    # non-zeros always take 40x.
+    # 60x/61x: weights in LDS; 41x: gathers SK samples ahead (tag table in LDS); 40x: one per
+    # sample. Rows of more than 128 non-zeros always take 40x.
     wide = int(np.max(np.diff(rp))) > 128
     if base is None:
         base = 600

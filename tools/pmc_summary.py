@@ -14,8 +14,9 @@ import json
 import os
 import statistics
 
-KERNELS = ("psgd::chain_block", "psgd::chain_sparse_spec", "psgd::chain_sparse", "psgd::chain_dense",
-           "psgd::chain_general", "psgd::fold_kernel", "psgd::margin_loss_kernel")
+KERNELS = ("psgd::chain_block", "psgd::chain_sparse_spec", "psgd::chain_sparse_lds", "psgd::chain_sparse",
+           "psgd::chain_dense", "psgd::chain_general", "psgd::fold_kernel", "psgd::fold_f32_kernel",
+           "psgd::wf32_init_kernel", "psgd::margin_loss_kernel")
 
 
 def short(name):
