@@ -38,31 +38,27 @@ namespace psgd {
 
 constexpr int LCAP = 128;                  // entries per row (two per lane)
 
-// The lanes of `pred`, plus lane 63.
-__device__ __forceinline__ uint64_t ballot_or63(bool pred) {
-    return __builtin_amdgcn_ballot_w64(pred) | (1ull << 63);
+// The chain's tail gathers and stores are buffer instructions over its fp32 vector: a 32-bit
+// byte offset per lane, and lanes without a tail entry get an out-of-range offset, which the
+// hardware bounds check turns into no access at all (loads return 0, stores are dropped). EXEC
+// stays full and every instruction counts once in vmcnt, with no per-lane 64-bit address or
+// EXEC juggling on the chain's critical path.
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+constexpr uint32_t kNoAccess = 0x80000000u;    // > any chain vector's byte size
+__device__ __forceinline__ i32x4 buffer_rsrc(const float* base, uint32_t bytes) {
+    const uint64_t a = (uint64_t)base;
+    // dword1: base[47:32], stride 0; dword2: num_records (bytes); dword3: raw dword access (gfx9)
+    return i32x4{__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)a),
+                 __builtin_amdgcn_readfirstlane((int32_t)((a >> 32) & 0xFFFF)),
+                 __builtin_amdgcn_readfirstlane((int32_t)bytes), 0x00020000};
 }
-// gather_sc1 / store_f32 (psgd_device.h) under an explicit EXEC mask; lanes outside `mask` keep
-// their destination register as it was.
-__device__ __forceinline__ float gather_sc1_masked(const float* p, uint64_t mask) {
+__device__ __forceinline__ float buffer_gather_sc1(i32x4 rsrc, uint32_t off) {
     float v;
-    uint64_t saved;
-    asm volatile(
-        "s_mov_b64 %1, exec\n\t"
-        "s_mov_b64 exec, %3\n\t"
-        "global_load_dword %0, %2, off sc1\n\t"
-        "s_mov_b64 exec, %1"
-        : "=&v"(v), "=&s"(saved) : "v"(p), "s"(mask) : "memory");
+    asm volatile("buffer_load_dword %0, %1, %2, 0 offen sc1" : "=v"(v) : "v"(off), "s"(rsrc) : "memory");
     return v;
 }
-__device__ __forceinline__ void store_f32_masked(float* p, float v, uint64_t mask) {
-    uint64_t saved;
-    asm volatile(
-        "s_mov_b64 %0, exec\n\t"
-        "s_mov_b64 exec, %3\n\t"
-        "global_store_dword %1, %2, off\n\t"
-        "s_mov_b64 exec, %0"
-        : "=&s"(saved) : "v"(p), "v"(v), "s"(mask) : "memory");
+__device__ __forceinline__ void buffer_store_f32(i32x4 rsrc, uint32_t off, float v) {
+    asm volatile("buffer_store_dword %0, %1, %2, 0 offen" : : "v"(v), "v"(off), "s"(rsrc) : "memory");
 }
 constexpr int kMetaRing = 128;             // rows of label / step / nnz
 constexpr int kSweepRows = 128;            // the tag table is swept once per this many rows
@@ -400,11 +396,9 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
     float loss_blk = 0.0f;
     int64_t count = 0;
     unsigned loaded = 0, tagged = 0;
-    // Target of masked-off gather / store lanes: 16 rotating 256-byte rows, a different one for
-    // each of the 4 VMEM instructions of 4 consecutive samples (accesses to one line from one
-    // wave are processed in order in L2; one shared dummy line serialised the chain's stream).
-    auto dummy = [&](int64_t t, int k) __attribute__((always_inline)) -> float* {
-        return V + d + 128 + (int)(((4 * t + k) & 15) << 6) + lane;
+    const i32x4 vrs = buffer_rsrc(V, (uint32_t)((int64_t)d * 4));   // the chain's vector [0, d)
+    auto boff = [](bool on, int32_t c) __attribute__((always_inline)) -> uint32_t {
+        return on ? (uint32_t)c << 2 : kNoAccess;
     };
     // gathered tail weights: row u's in gr[u % (SK + 1)]. A gather's registers are written by
     // the load when it lands, so they are never copied before their s_waitcnt: the gather of
@@ -427,13 +421,11 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
         const int nz = meta->nnz[u & (kMetaRing - 1)];
         return GCols{sl.col[lane], sl.col[lane + 64], nz};
     };
-    // Only tail entries touch memory: the other lanes are masked off (lane 63 always runs, on a
-    // dummy address when it has no tail entry, so no instruction has an empty EXEC and each
-    // still counts once in vmcnt); a scattered VMEM instruction costs its issue per address.
-    auto gather = [&](const GCols& G, float (&g)[2], int64_t t) __attribute__((always_inline)) {
+    // Only tail entries touch memory: the other lanes get the no-access offset.
+    auto gather = [&](const GCols& G, float (&g)[2]) __attribute__((always_inline)) {
         const bool a0 = lane < G.nnz && G.c0 >= K, a1 = lane + 64 < G.nnz && G.c1 >= K;
-        g[0] = gather_sc1_masked(a0 ? V + G.c0 : dummy(t, 0), ballot_or63(a0));
-        g[1] = gather_sc1_masked(a1 ? V + G.c1 : dummy(t, 1), ballot_or63(a1));
+        g[0] = buffer_gather_sc1(vrs, boff(a0, G.c0));
+        g[1] = buffer_gather_sc1(vrs, boff(a1, G.c1));
     };
     // the data of sample t
     struct Row { float x0, x1; uint32_t rw0, rw1; int32_t c0, c1; int nnz; float y, s; double s64; };
@@ -443,16 +435,16 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
         return Row{sl.val[lane], sl.val[lane + 64], sl.rw[lane], sl.rw[lane + 64], sl.col[lane],
                    sl.col[lane + 64], meta->nnz[m], meta->y[m], meta->s[m], L2 ? meta->s64[m] : 0.0};
     };
-    // prologue: gathers of rows 0 .. SK-1, each followed by two (dummy) stores, the same VMEM
+    // prologue: gathers of rows 0 .. SK-1, each followed by two no-access stores, the same VMEM
     // pattern as a sample of the loop; then the columns of row SK and the data of sample 0
     GCols gc{0, 0, 0};
     if constexpr (TAIL) {
         static_for<SK>([&](auto qc) {
             constexpr int q = decltype(qc)::value;
             need(q + 1, 0);
-            gather(gcols(q), gr[q], q);
-            store_f32(dummy(q, 2), 0.0f);
-            store_f32(dummy(q, 3), 0.0f);
+            gather(gcols(q), gr[q]);
+            buffer_store_f32(vrs, kNoAccess, 0.0f);
+            buffer_store_f32(vrs, kNoAccess, 0.0f);
         });
         need(SK + 1, 1);
         gc = gcols(SK);
@@ -473,7 +465,7 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
         const float l0 = lds[r0], l1 = lds[r1];
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (TAIL) {
-            gather(gc, gr[QN], t);
+            gather(gc, gr[QN]);
             gc = gcols(t + SK + 1);
         }
         const Row nxt = row_of(t + 1);
@@ -512,8 +504,8 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
         // this row's tail stores (2 VMEM instructions)
         if constexpr (TAIL) {
             const bool a0 = lane < cur.nnz && cur.c0 >= K, a1 = lane + 64 < cur.nnz && cur.c1 >= K;
-            store_f32_masked(a0 ? V + cur.c0 : dummy(t, 2), nv0, ballot_or63(a0));
-            store_f32_masked(a1 ? V + cur.c1 : dummy(t, 3), nv1, ballot_or63(a1));
+            buffer_store_f32(vrs, boff(a0, cur.c0), nv0);
+            buffer_store_f32(vrs, boff(a1, cur.c1), nv1);
         }
         publish(&hdr->done, t + 1);
         cur = nxt;

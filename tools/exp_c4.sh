@@ -21,5 +21,8 @@ for v in ${VARIANTS:-lds4 lds8 lds4_d4k lds8_d4k}; do
     lds4_h10k) run $v PSGD_SPARSE_KERNEL=lds PSGD_SPARSE_LDS_HEAD=10000 PSGD_STAMPS=1 ;;
     lds8_h10k) run $v PSGD_SPARSE_KERNEL=lds PSGD_SPARSE_LDS_HEAD=10000 PSGD_SPARSE_SK=8 PSGD_STAMPS=1 ;;
     lds4_d30k) EXTRA="--features 30000" run $v PSGD_SPARSE_KERNEL=lds PSGD_STAMPS=1 ;;
+    lds4_d4k_h1364) EXTRA="--features 4096" run $v PSGD_SPARSE_KERNEL=lds PSGD_SPARSE_LDS_HEAD=1364 PSGD_STAMPS=1 ;;
+    lds4_d4k_h4000) EXTRA="--features 4096" run $v PSGD_SPARSE_KERNEL=lds PSGD_SPARSE_LDS_HEAD=4000 PSGD_STAMPS=1 ;;
+    lds4_h2000) run $v PSGD_SPARSE_KERNEL=lds PSGD_SPARSE_LDS_HEAD=2000 PSGD_STAMPS=1 ;;
   esac
 done
