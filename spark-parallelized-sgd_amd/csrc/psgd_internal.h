@@ -107,6 +107,12 @@ bool sparse_lds_applies(int64_t d, int64_t max_nnz);
 int64_t sparse_lds_head(int64_t d);
 int launch_sparse_lds_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
                              int updater, int64_t max_nnz, hipStream_t stream, int* kernel_variant);
+// The fp32 CSR kernel as a batched scalar recurrence over sparse Gram terms
+// (psgd_sparse_gram.hip): rows of <= 128 non-zeros, features [0, K) in LDS and [K, d) in L.wf32.
+bool sparse_gram_applies(int64_t d, int64_t max_nnz);
+int64_t sparse_gram_head(int64_t d);
+int launch_sparse_gram_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
+                              int updater, int64_t max_nnz, hipStream_t stream, int* kernel_variant);
 // Longest row of a device-resident CSR partition (synchronises `st`).
 int csr_max_nnz(const int64_t* d_row_ptr, int64_t n, int64_t* out, hipStream_t st);
 // RDD.sample(false, fraction, seed) per partition (PSGD.scala:242): from the registered

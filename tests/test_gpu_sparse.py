@@ -1,6 +1,7 @@
 """The fp32 CSR chain kernels (psgd_sparse_lds.hip, psgd_sparse.hip) against the fp64 CPU oracle.
 
-Every case runs on each kernel variant (PSGD_SPARSE_KERNEL forces one): chain_sparse_lds with
+Every case runs on each kernel variant (PSGD_SPARSE_KERNEL forces one): chain_sparse_gram (the
+batched Gram recurrence) with all weights in LDS and with an LDS head of d/3, chain_sparse_lds with
 all weights in LDS, with an LDS head of d/3 features and the rest in HBM (PSGD_SPARSE_LDS_HEAD:
 exercises the tail gathers and their corrections at small d) at speculation depths 4 and 8,
 chain_sparse_spec, and chain_sparse.
@@ -35,6 +36,8 @@ def need_gpu():
 
 
 KERNELS = {  # name: (environment, variant base without the storage digit)
+    "gram": ({"PSGD_SPARSE_KERNEL": "gram"}, 630),
+    "gram_tail": ({"PSGD_SPARSE_KERNEL": "gram", "PSGD_SPARSE_LDS_HEAD": "third"}, 630),
     "lds": ({"PSGD_SPARSE_KERNEL": "lds"}, 600),
     "lds_tail": ({"PSGD_SPARSE_KERNEL": "lds", "PSGD_SPARSE_LDS_HEAD": "third"}, 600),
     "lds_tail_sk8": ({"PSGD_SPARSE_KERNEL": "lds", "PSGD_SPARSE_LDS_HEAD": "third", "PSGD_SPARSE_SK": "8"}, 610),
@@ -86,7 +89,7 @@ def check(pkg, oracle, rp, col, val, y, d, offs, grad, upd, step, reg, iters, fr
     w, h, counts = pkg.runParallelizedSGD(data, getattr(pkg, G[grad])(), getattr(pkg, U[upd])(), step,
                                           iters, reg, frac, np.zeros(d), 0.0, compute_dtype="f32",
                                           return_chain_counts=True)
-    # 60x/61x: weights in LDS; 41x: gathers SK samples ahead (tag table in LDS); 40x: one per
+    # 63x: Gram recurrence; 60x/61x: weights in LDS; 41x: gathers SK samples ahead (tag table in LDS); 40x: one per
     # sample. Rows of more than 128 non-zeros always take 40x.
     wide = int(np.max(np.diff(rp))) > 128
     if base is None:
