@@ -904,8 +904,8 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         return e && *e && *e != '0';
     }();
     if (want_stamps && layout == psgd::kCsr) {
-        HIP_TRY(ctx->stamps.ensure((size_t)P * 8 * sizeof(unsigned long long)));
-        HIP_TRY(hipMemsetAsync(ctx->stamps.p, 0, (size_t)P * 8 * sizeof(unsigned long long), st));
+        HIP_TRY(ctx->stamps.ensure((size_t)P * 16 * sizeof(unsigned long long)));
+        HIP_TRY(hipMemsetAsync(ctx->stamps.p, 0, (size_t)P * 16 * sizeof(unsigned long long), st));
         L.stamps = ctx->stamps.as<unsigned long long>();
     }
     L.zbuf = nullptr;
@@ -976,21 +976,22 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         if (L.stamps) {   // PSGD_STAMPS=1: per-chain cycle counters of the CSR fp32 kernels (stderr)
             // chain_sparse_gram: {chain, loader, gram, apply} x {total, waiting}; chain_sparse_lds:
             // {chain, loader, tagger} x {total, waiting}; chain_sparse_spec: {chain, helper} x ...
-            const int KS = ctx->last_variant >= 630 ? 8 : ctx->last_variant >= 600 ? 6 : 4;
-            std::vector<unsigned long long> h((size_t)P * 8);
+            const int KS = ctx->last_variant >= 630 ? 16 : ctx->last_variant >= 600 ? 6 : 4;
+            std::vector<unsigned long long> h((size_t)P * 16);
             HIP_TRY(hipMemcpyAsync(h.data(), L.stamps, h.size() * 8, hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
-            std::vector<double> v[8];
+            std::vector<double> v[16];
             for (int p = 0; p < P; ++p)
                 for (int k = 0; k < KS; ++k)
                     v[k].push_back((double)h[(size_t)p * KS + k] / std::max<int64_t>(n_max, 1));
             const char* n4[4] = {"chain.total", "chain.wait", "helper.total", "helper.wait"};
             const char* n6[6] = {"chain.total", "chain.wait", "loader.total", "loader.wait", "tagger.total", "tagger.wait"};
-            const char* n8[8] = {"chain.total", "chain.wait", "loader.total", "loader.wait", "gram.total", "gram.wait",
-                                 "apply.total", "apply.wait"};
+            const char* n8[16] = {"chain.total", "chain.wait", "loader.total", "loader.wait", "gram.total", "gram.wait",
+                                  "apply.total", "apply.wait", "gram.phaseA", "gram.phaseB", "gram.items", "gram.iters",
+                                  "apply.update", "apply.copy", "apply.dots", "apply.vmwait"};
             for (int k = 0; k < KS; ++k) {
                 std::sort(v[k].begin(), v[k].end());
-                fprintf(stderr, "psgd stamps %-18s cycles/row median %8.1f\n", KS == 8 ? n8[k] : KS == 6 ? n6[k] : n4[k],
+                fprintf(stderr, "psgd stamps %-18s cycles/row median %8.1f\n", KS == 16 ? n8[k] : KS == 6 ? n6[k] : n4[k],
                         v[k][v[k].size() / 2]);
             }
         }

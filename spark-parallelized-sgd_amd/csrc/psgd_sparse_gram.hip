@@ -58,8 +58,8 @@ constexpr uint32_t kRowMask = 0xFFFFFF;
 constexpr uint32_t kTagValid = 0x80000000u;
 constexpr int kMaxHops = GPR * GCAP;  // a walk visits every window entry at most once
 constexpr uint32_t kNoAccessG = 0x80000000u;   // buffer offset past any chain vector
-constexpr int kBmLog = 16;
-constexpr int kBmBits = 1 << kBmLog;  // presence bitmap bits per plane (features, hashed past this)
+constexpr int kStampLog = 14;
+constexpr int kStampN = 1 << kStampLog;   // presence stamps (hashed features)
 constexpr int kQCap = 1024;           // gram work queue items (a batch's entries)
 
 struct GHeader {
@@ -91,12 +91,12 @@ struct GFixed {
     float G[GRB][GB][2 * GB];     // G[t][0..7]: rows of batch b-1; G[t][8..15]: batch b
     uint32_t link[GPR][GCAP];     // the tag each entry's insertion displaced
     uint32_t bucket[HSIZE];       // latest tag per bucket (0 = empty)
-    uint32_t bm[kBmBits / 16];    // presence bitmap: 2 bits per feature (even / odd batch planes)
+    uint8_t stamp[kStampN];       // presence: batch number (mod 256) of the latest entry per hashed feature
     uint64_t queue[kQCap];        // gram work items: {link, row slot / entry / batch row}
     GSlot slot[GSR];
 };
 static_assert(sizeof(GFixed) % 16 == 0 && offsetof(GFixed, G) % 16 == 0 && offsetof(GFixed, slot) % 16 == 0 &&
-                  offsetof(GFixed, bm) % 8 == 0 && offsetof(GFixed, queue) % 8 == 0,
+                  offsetof(GFixed, stamp) % 8 == 0 && offsetof(GFixed, queue) % 8 == 0,
               "LDS alignment");
 constexpr int64_t kGLdsCap = 160 * 1024;
 
@@ -159,7 +159,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     constexpr unsigned kLink = (unsigned)(offsetof(GFixed, link) / 4);
     constexpr unsigned kBucket = (unsigned)(offsetof(GFixed, bucket) / 4);
     constexpr unsigned kG = (unsigned)(offsetof(GFixed, G) / 4);
-    constexpr unsigned kBm = (unsigned)(offsetof(GFixed, bm) / 4);
     constexpr unsigned kQueue = (unsigned)(offsetof(GFixed, queue) / 4);
     float* W = lds + kW;
 
@@ -174,7 +173,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     float* V = L.wf32 + (int64_t)chain * L.wstride;
 
     for (int i = threadIdx.x; i < HSIZE; i += blockDim.x) F->bucket[i] = 0u;
-    for (int i = threadIdx.x; i < kBmBits / 16; i += blockDim.x) F->bm[i] = 0u;
+    for (int i = threadIdx.x; i < kStampN / 4; i += blockDim.x) reinterpret_cast<uint32_t*>(F->stamp)[i] = 0x80808080u;
     for (int i = threadIdx.x; i < K; i += blockDim.x) W[i] = float(as_global(L.w_in)[i]);
     if (threadIdx.x < 64) {
         F->dread[threadIdx.x] = 0.0f;
@@ -184,6 +183,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     __syncthreads();
 
     uint64_t st_wait = 0;                      // diagnostic (PSGD_STAMPS): cycles spent waiting
+    uint64_t st_x[4] = {0, 0, 0, 0};           // diagnostic: per-wave sub-phase cycles / counts
+    const bool stamps = L.stamps != nullptr;
+    auto tick = [&]() __attribute__((always_inline)) -> uint64_t { return stamps ? __builtin_amdgcn_s_memtime() : 0; };
     const uint64_t st_begin = __builtin_amdgcn_s_memtime();
     // The flags live in LDS and are reached through an explicit address-space-3 view: a generic
     // pointer would compile to flat accesses, which count on vmcnt and make every poll and publish
@@ -323,18 +325,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
     } else if (wave == 2) {
         // ---------------- gram: link the batch's entries, walk the links, accumulate G ----------
-        // Per batch b, rows in order: each entry tests the presence bitmap of the window (a bit per
-        // feature -- hashed past 65,536 features -- in two planes, batches of even / odd index),
-        // sets its own bit, and links itself into its bucket by an exchange. Only an entry whose
+        // Per batch b, rows in order: each entry tests the presence stamp of its (hashed) feature
+        // -- the batch number, mod 256, of the feature's latest entry: present in the window if it
+        // names batch b-1 or b (a stale or shared stamp only costs a walk) -- stamps it with b,
+        // and links itself into its bucket by an exchange. Only an entry whose
         // feature is present elsewhere in the window and whose link points into the window walks:
         // it goes into an LDS work queue, which the wave drains 64 items per step (one hop each;
         // an item still inside the window goes back into the queue).
         unsigned loaded = 0, cd = 0;
-        // batch b-1's bitmap bits, (dword << 5) | bit, bit 31 = none (cleared after batch b)
-        uint32_t pbit[2 * GB];
-#pragma unroll
-        for (int q = 0; q < 2 * GB; ++q) pbit[q] = 0x80000000u | ((kDwrite + lane) << 5);
-        const bool exact_bits = d <= kBmBits;
         for (int64_t b = 0; b < nb; ++b) {
             if (!wait_for(loaded, kLoaded, GB * b + GB, 32)) break;
             // G[b % GRB] held batch b - GRB, which the chain has finished with
@@ -342,8 +340,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             const unsigned gbase = kG + (unsigned)(b & (GRB - 1)) * (GB * 2 * GB);
             lds[gbase + 2 * lane] = 0.0f;
             lds[gbase + 2 * lane + 1] = 0.0f;
-            const unsigned plane = (unsigned)(b & 1);
+            const uint32_t bs = (uint32_t)b & 255u, bp = (uint32_t)(b - 1) & 255u;
+            typedef __attribute__((address_space(3))) volatile uint8_t lbyte;
+            lbyte* SB = (lbyte*)(smem);
             uint32_t qt = 0;             // queue tail (items ever queued this batch)
+            const uint64_t tA = tick();
             // the batch's columns and row lengths (one LDS round trip)
             int32_t cl[2 * GB];
             int nz[GB];
@@ -355,10 +356,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                 cl[2 * i] = sl.col[lane];
                 cl[2 * i + 1] = sl.col[lane + 64];
             }
-            uint32_t nbit[2 * GB], bmw[2 * GB], lk[2 * GB];
+            uint32_t sv[2 * GB], lk[2 * GB];
             // issue, rows in order (one wave's LDS operations execute in program order): the
-            // presence test, the entry's own bit, its link; lanes without an entry use their
-            // dummy dwords
+            // presence test (the feature's stamp names batch b-1 or b), the entry's own stamp, its
+            // link; lanes without an entry use their dummy dwords
 #pragma unroll
             for (int q = 0; q < 2 * GB; ++q) {
                 const int i = q >> 1;
@@ -366,14 +367,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                 const int64_t u = GB * b + i;
                 const bool on = e < nz[i];
                 const int32_t c = cl[q];
-                // two bits per feature (planes of even / odd batches), 16 features per dword
-                const uint32_t k = exact_bits ? (uint32_t)c : ((uint32_t)c * 2654435761u) >> (32 - kBmLog);
-                const unsigned word = on ? kBm + (k >> 4) : kDread + lane;
-                const uint32_t sh = 2 * (k & 15);
-                bmw[q] = ldsu[word];
-                nbit[q] = on ? (word << 5) | (sh + plane) : 0x80000000u | ((kDwrite + lane) << 5);
-                __hip_atomic_fetch_or(ldsu + (on ? word : kDwrite + lane), on ? 1u << (sh + plane) : 0u,
-                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const uint32_t k = ((uint32_t)c * 2654435761u) >> (32 - kStampLog);
+                const unsigned sb = on ? (unsigned)offsetof(GFixed, stamp) + k : 4 * (kDwrite + lane);
+                sv[q] = SB[sb];
+                SB[sb] = (uint8_t)bs;
                 const uint32_t tag = kTagValid | (((uint32_t)u & kRowMask) << 7) | (uint32_t)e;
                 lk[q] = __hip_atomic_exchange(ldsu + (on ? kBucket + hash_of(c) : kDwrite + lane), tag,
                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -388,7 +385,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                 const bool on = e < nz[i];
                 const uint32_t l = on ? lk[q] : 0u;
                 F->link[u & (GPR - 1)][e] = l;
-                const bool pres = ((bmw[q] >> ((nbit[q] & 31u) & ~1u)) & 3u) != 0u;
+                const bool pres = sv[q] == bs || sv[q] == bp;
                 const bool act = on && pres && l != 0u && (int)(((uint32_t)u - (l >> 7)) & kRowMask) <= wlim;
                 const uint64_t mk = __builtin_amdgcn_ballot_w64(act);
                 if (mk) {
@@ -402,11 +399,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                     qt += (uint32_t)__builtin_popcountll(mk);
                 }
             }
+            const uint64_t tB = tick();
+            if (stamps) { st_x[0] += tB - tA; st_x[2] += qt; }
             // drain: one hop per item; a link to the same feature in an earlier row adds x_t x_r
             // to G[t][r]; an item whose next link stays inside the window (at non-decreasing
             // distance) is queued again
             uint32_t qh = 0;
             for (int it = 0; qh < qt && it < kMaxHops; ++it) {
+                if (stamps) st_x[3] += 1;
                 const uint32_t take = qt - qh < 64u ? qt - qh : 64u;
                 const bool my = (uint32_t)lane < take;
                 const uint64_t item = *reinterpret_cast<const uint64_t*>(
@@ -444,14 +444,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                     qt += (uint32_t)__builtin_popcountll(mk);
                 }
             }
-            // batch b-1 leaves the window: clear its plane for batch b+1
-#pragma unroll
-            for (int q = 0; q < 2 * GB; ++q) {
-                const uint32_t m = (pbit[q] >> 31) ? 0u : 1u << (pbit[q] & 31);
-                __hip_atomic_fetch_and(ldsu + ((pbit[q] >> 5) & 0x3FFFFFu), ~m, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-                pbit[q] = nbit[q];
-            }
+            if (stamps) st_x[1] += tick() - tB;
             publish(kGram, b + 1);
         }
     } else if (wave == 3) {
@@ -493,7 +486,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                                "+v"(wt[12]), "+v"(wt[13]), "+v"(wt[14]), "+v"(wt[15])
                              :
                              : "memory");
-                if (L.stamps) st_wait += __builtin_amdgcn_s_memtime() - vm0;
+                if (L.stamps) { st_wait += __builtin_amdgcn_s_memtime() - vm0; st_x[3] += __builtin_amdgcn_s_memtime() - vm0; }
             }
             float part[GB];
 #pragma unroll
@@ -539,13 +532,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
         auto step = [&](int64_t b, Set& St) __attribute__((always_inline)) -> bool {
             if (!wait_for(cd, kCdone, b + 1, 64)) return false;
+            const uint64_t t0 = tick();
             update(b, St);
+            const uint64_t t1 = tick();
+            if (stamps) st_x[0] += t1 - t0;
             if (b + 2 < nb) {
                 if (!wait_for(loaded, kLoaded, GB * (b + 3), 64)) return false;
+                const uint64_t t2 = tick();
                 copy(b + 2, St);
                 publish(kGathered, b + 3);
+                const uint64_t t3 = tick();
                 dots(b + 2, St);
                 publish(kPdone, b + 3);
+                if (stamps) { st_x[1] += t3 - t2; st_x[2] += tick() - t3; }
             }
             return true;
         };
@@ -618,8 +617,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if (!ok) FL[kStop] = 1u;
     }
     if (L.stamps && lane == 0) {
-        L.stamps[(size_t)chain * 8 + 2 * wave] = __builtin_amdgcn_s_memtime() - st_begin;
-        L.stamps[(size_t)chain * 8 + 2 * wave + 1] = st_wait;
+        L.stamps[(size_t)chain * 16 + 2 * wave] = __builtin_amdgcn_s_memtime() - st_begin;
+        L.stamps[(size_t)chain * 16 + 2 * wave + 1] = st_wait;
+        if (wave >= 2)
+            for (int k = 0; k < 4; ++k) L.stamps[(size_t)chain * 16 + 8 + 4 * (wave - 2) + k] = st_x[k];
     }
     __syncthreads();
 
