@@ -109,50 +109,13 @@ __host__ __device__ constexpr int row_lane64(int i) {
 // SGDUpdater.scala:95 / :178 axpy(-thisIterStepSize, gradient, w)).
 //   Logistic: mult = 1/(1 + exp(-z)) - y;  LeastSquares: mult = z - y;
 //   Hinge: mult = 1 > ls*z ? -ls : 0 (ls = 2y - 1; the empty gradient adds nothing)
-// The recurrence's exp and division are its latency (8 of them in sequence per block), so both
-// are short dependent chains here instead of OCML's exp and the IEEE division sequence:
-//   exp(x) = 2^k p(r), k = rint(x / ln 2), r = x - k ln 2 (two-part ln 2), |r| <= 0.347, p the
-//   degree-13 Taylor polynomial by Estrin's scheme (truncation < 4e-18 relative), v_ldexp_f64
-//   (overflow to inf, underflow to 0 / subnormal as the exact result rounds);
-//   1 / d = v_rcp_f64 refined by two Newton steps (quadratic: ~1 ulp), 0 for d = inf.
-// Both stay within a few ulp of the correctly rounded results, far inside the fp64 mode's 1e-9
-// bar.
-__device__ __forceinline__ double exp_fast64(double x) {
-    const double xc = __builtin_fmin(__builtin_fmax(x, -1100.0), 1100.0);
-    const double kd = __builtin_rint(xc * 1.4426950408889634);
-    double r = __builtin_fma(-kd, 6.93147180369123816490e-01, xc);   // ln 2 high part (exact k * hi)
-    r = __builtin_fma(-kd, 1.90821492927058770002e-10, r);            // ln 2 low part
-    const double r2 = r * r, r4 = r2 * r2, r8 = r4 * r4;
-    const double a0 = 1.0 + r;
-    const double a1 = __builtin_fma(r, 1.0 / 6, 0.5);
-    const double a2 = __builtin_fma(r, 1.0 / 120, 1.0 / 24);
-    const double a3 = __builtin_fma(r, 1.0 / 5040, 1.0 / 720);
-    const double a4 = __builtin_fma(r, 1.0 / 362880, 1.0 / 40320);
-    const double a5 = __builtin_fma(r, 1.0 / 39916800, 1.0 / 3628800);
-    const double a6 = __builtin_fma(r, 1.0 / 6227020800.0, 1.0 / 479001600);
-    const double b0 = __builtin_fma(r2, a1, a0);
-    const double b1 = __builtin_fma(r2, a3, a2);
-    const double b2 = __builtin_fma(r2, a5, a4);
-    const double c0 = __builtin_fma(r4, b1, b0);
-    const double c1 = __builtin_fma(r4, a6, b2);
-    const double p = __builtin_fma(r8, c1, c0);
-    const double e = __builtin_amdgcn_ldexp(p, (int)kd);
-    return x != x ? x : e;
-}
-__device__ __forceinline__ double recip_fast64(double d) {
-    double y = __builtin_amdgcn_rcp(d);
-    y = __builtin_fma(y, __builtin_fma(-d, y, 1.0), y);
-    y = __builtin_fma(y, __builtin_fma(-d, y, 1.0), y);
-    return __builtin_isinf(d) ? 0.0 : y;
-}
-
 template <int GRAD>
 __device__ __forceinline__ double coef64(double z, double y, double ns) {
     if constexpr (GRAD == G_LEAST_SQUARES) {
         return ns * (z - y);
     } else if constexpr (GRAD == G_LOGISTIC) {
         const double margin = -z;
-        return ns * (recip_fast64(1.0 + exp_fast64(margin)) - y);
+        return ns * ((1.0 / (1.0 + exp(margin))) - y);
     } else {
         const double ls = 2.0 * y - 1.0;
         return (1.0 > ls * z) ? ns * (-ls) : 0.0;
