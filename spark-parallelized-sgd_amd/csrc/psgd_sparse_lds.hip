@@ -327,22 +327,43 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
             // sweep the chunks of rows u0 .. u0 + TB - 1, keeping the tags of rows u0 - SK .. u0 - 1
             // (the oldest rows this step's lookups need); each chunk is swept at least every
             // kSweepRows rows, so no tag outlives 256 rows
+            auto sweep4 = [&](uint64_t v) __attribute__((always_inline)) -> uint64_t {
+                uint64_t o = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const unsigned tg = (unsigned)(v >> (16 * k)) & 0xFFFF;
+                    const unsigned dl = ((unsigned)u0 - (tg >> 8)) & 255;
+                    const bool live = tg != 0xFFFF && dl >= 1 && dl <= SK;
+                    o |= (uint64_t)(live ? tg : 0xFFFFu) << (16 * k);
+                }
+                return o;
+            };
+            if (chunk <= 256) {
+                // one 4-tag word per lane and row: the TB reads share one LDS round trip
+                uint64_t sv[TB];
+                bool sok[TB];
+                int64_t si[TB];
+#pragma unroll
+                for (int q = 0; q < TB; ++q) {
+                    const int64_t lo = ((u0 + q) & (kSweepRows - 1)) * chunk;
+                    const int64_t hi = lo + chunk < T ? lo + chunk : T;
+                    si[q] = lo + 4 * lane;
+                    sok[q] = si[q] < hi;
+                    sv[q] = *reinterpret_cast<const uint64_t*>(tagpos + (sok[q] ? si[q] : 0));
+                }
+#pragma unroll
+                for (int q = 0; q < TB; ++q)
+                    if (sok[q]) *reinterpret_cast<uint64_t*>(tagpos + si[q]) = sweep4(sv[q]);
+            } else {
 #pragma unroll
             for (int q = 0; q < TB; ++q) {
                 const int64_t lo = ((u0 + q) & (kSweepRows - 1)) * chunk;
                 const int64_t hi = lo + chunk < T ? lo + chunk : T;
                 for (int64_t i = lo + 4 * lane; i < hi; i += 256) {
                     const uint64_t v = *reinterpret_cast<const uint64_t*>(tagpos + i);
-                    uint64_t o = 0;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const unsigned tg = (unsigned)(v >> (16 * k)) & 0xFFFF;
-                        const unsigned dl = ((unsigned)u0 - (tg >> 8)) & 255;
-                        const bool live = tg != 0xFFFF && dl >= 1 && dl <= SK;
-                        o |= (uint64_t)(live ? tg : 0xFFFFu) << (16 * k);
-                    }
-                    *reinterpret_cast<uint64_t*>(tagpos + i) = o;
+                    *reinterpret_cast<uint64_t*>(tagpos + i) = sweep4(v);
                 }
+            }
             }
             unsigned va[TB], vb[TB];
 #pragma unroll
