@@ -35,6 +35,8 @@
 // No MFMA: the triangle is 3.5 dots per row (an f64 16x16x4 MFMA tile would spend 16).
 #include "psgd_device.h"
 
+#include <type_traits>
+
 namespace psgd {
 
 namespace {
@@ -145,6 +147,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     constexpr int E = NV * VEC;            // features per lane
     constexpr int ROW_BYTES = NV * 1024;
     constexpr bool KEEP = E <= 8;          // the chain wave keeps a block's rows in registers
+    // f32 rows of up to 16 features per lane: kept in registers as stored (128 VGPRs) and
+    // converted where used, so a block's rows leave LDS once, in one batch
+    constexpr bool RAW = !KEEP && std::is_same<S, float>::value && E <= 16;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // LDS: [RingHeader 16 B][GramHeader64 16 B][meta ring MB x 256 B][Gram ring GS x 512 B]
     //      [row ring R x ROW_BYTES]
@@ -223,12 +228,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
         unsigned ready = 0;
         unsigned done = 0;
+        PSGD_STAMP(const uint64_t st_begin = __builtin_amdgcn_s_memtime(); uint64_t st_rd = 0;)
         int rs = gw * kB;            // ring slot of the block's first row (R is a multiple of 16)
         int gs = gw;                 // Gram slot of the block
         for (int64_t b = gw; b < nblk; b += 2) {
             const int64_t t0 = b * kB;
             const int64_t kk = (n - t0) < kB ? (n - t0) : kB;
+            PSGD_STAMP(const uint64_t st_w = __builtin_amdgcn_s_memtime();)
             if (!wait_ready(ready, t0 + kk, 4)) break;
+            PSGD_STAMP(st_rd += __builtin_amdgcn_s_memtime() - st_w;)
             const char* base = ring + rs * ROW_BYTES;
             rs += 2 * kB;
             if (rs >= R) rs -= R;
@@ -266,6 +274,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             ++done;
             __hip_atomic_store(&ghdr->gdone[gw], done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
+        PSGD_STAMP(if (L.stamps && lane == 0) {
+            unsigned long long* o = L.stamps + (size_t)chain * 16 + 8 + 4 * gw;
+            o[0] = __builtin_amdgcn_s_memtime() - st_begin; o[1] = st_rd;
+        })
         return;
     }
 
@@ -294,6 +306,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     int rs = 0, gs = 0, ms = 0;      // ring slot, Gram slot and meta block of the current block
     const int64_t nfull = n / kB;
     const int ntail = (int)(n - nfull * kB);
+    PSGD_STAMP(const uint64_t st_begin = __builtin_amdgcn_s_memtime(); uint64_t st_rd = 0, st_gr = 0, st_p = 0, st_rec = 0, st_upd = 0;)
 
     auto wait_rows = [&](int64_t rows) __attribute__((always_inline)) -> bool {
         return wait_ready(ready, rows, 2);
@@ -313,7 +326,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
     };
 
-    // One block: rows in xr (KEEP) or in the ring at `base`; kk rows (kB unless TAIL).
+    V xraw[kB][RAW ? NV : 1];
+    // A block's rows from the ring into registers as stored; rows >= kk (a tail block) are zero.
+    auto load_raw = [&](auto tail_c, const char* base, int kk) __attribute__((always_inline)) {
+        constexpr bool TAIL = decltype(tail_c)::value;
+        if constexpr (RAW) {
+#pragma unroll
+            for (int k = 0; k < kB; ++k) {
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    V xv = *reinterpret_cast<const V*>(base + k * ROW_BYTES + v * 1024 + lane * 16);
+                    if constexpr (!FULL) {
+                        if ((v * 64 + lane) * VEC >= dsc.ld) xv = V(0);
+                    }
+                    xraw[k][v] = (TAIL && k >= kk) ? V(0) : xv;
+                }
+            }
+        }
+    };
+    // One block: rows in xr (KEEP), in xraw (RAW) or in the ring at `base`; kk rows (kB unless TAIL).
     auto block = [&](auto tail_c, double (&xr)[kB][E], int64_t b, int kk, const char* base)
                      __attribute__((always_inline)) -> bool {
         constexpr bool TAIL = decltype(tail_c)::value;
@@ -321,7 +352,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         // this lane's row: label and stepSize/sqrt(j)
         const f64x2 meta = *reinterpret_cast<const f64x2*>(
             meta_ring + ms * kMetaBlockBytes + ((int)(b & 1) * kB + krow) * 16);
-        if constexpr (KEEP) {
+        if constexpr (KEEP || RAW) {
             // rows are in registers (the Gram and meta slots are reused only after the next
             // block is handed back): free the ring slots (the loader also waits for the Gram)
             __hip_atomic_store(&hdr->consumed, (unsigned)(t0 + kk), __ATOMIC_RELAXED,
@@ -330,6 +361,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         // flags this block tests, read now so that their LDS round trip lands under the dots
         const unsigned gpre = __hip_atomic_load(&ghdr->gdone[b & 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const unsigned rpre = __hip_atomic_load(&hdr->ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        PSGD_STAMP(const uint64_t st_a = __builtin_amdgcn_s_memtime();)
         // p_k = x_k . W
         double pk[kB];
 #pragma unroll
@@ -338,6 +370,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             if constexpr (KEEP) {
 #pragma unroll
                 for (int e = 0; e < E; ++e) a = __builtin_fma(xr[k][e], w[e], a);
+            } else if constexpr (RAW) {
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    double xv[VEC];
+                    unpack<S, double>(xraw[k][v], xv);
+#pragma unroll
+                    for (int h = 0; h < VEC; ++h) a = __builtin_fma(xv[h], w[v * VEC + h], a);
+                }
             } else {
 #pragma unroll
                 for (int v = 0; v < NV; ++v) {
@@ -353,6 +393,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         const double nsv = -sv;
         const double alpha = 1.0 - sv * lam;      // SquaredL2 shrink of this lane's row (UPD:169)
         double z = reduce8d(pk, lane);
+        PSGD_STAMP(const uint64_t st_b = __builtin_amdgcn_s_memtime(); st_p += st_b - st_a;)
         // the block's Gram triangle (Gram wave b&1 publishes its blocks in order)
         {
             const unsigned need = (unsigned)(b >> 1) + 1;
@@ -368,6 +409,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                 }
             }
         }
+        PSGD_STAMP(const uint64_t st_g = __builtin_amdgcn_s_memtime(); st_gr += st_g - st_b;)
         const double* grow = gring + gs * (kB * kB) + krow * kB;
         double G[kB];
 #pragma unroll
@@ -403,6 +445,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
         count += kk;
         if (rpre > ready) ready = rpre;
+        PSGD_STAMP(const uint64_t st_c = __builtin_amdgcn_s_memtime(); st_rec += st_c - st_g;)
 
         // W <- a_i W + c_i x_i, i = 0..kk-1, in sample order
 #pragma unroll
@@ -412,6 +455,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                 for (int e = 0; e < E; ++e) {
                     if constexpr (UPD == U_SQUARED_L2) w[e] = __builtin_fma(c[i], xr[i][e], w[e] * al[i]);
                     else w[e] = __builtin_fma(c[i], xr[i][e], w[e]);
+                }
+            } else if constexpr (RAW) {
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    double xv[VEC];
+                    unpack<S, double>(xraw[i][v], xv);
+#pragma unroll
+                    for (int h = 0; h < VEC; ++h) {
+                        const int e = v * VEC + h;
+                        if constexpr (UPD == U_SQUARED_L2) w[e] = __builtin_fma(c[i], xv[h], w[e] * al[i]);
+                        else w[e] = __builtin_fma(c[i], xv[h], w[e]);
+                    }
                 }
             } else if (!TAIL || i < kk) {
 #pragma unroll
@@ -427,10 +482,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                 }
             }
         }
-        if constexpr (!KEEP) {
+        if constexpr (!KEEP && !RAW) {
             __hip_atomic_store(&hdr->consumed, (unsigned)(t0 + kk), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
         }
+        PSGD_STAMP(st_upd += __builtin_amdgcn_s_memtime() - st_c;)
         rs += kB;
         if (rs == R) rs = 0;
         if (++gs == GS) gs = 0;
@@ -443,19 +499,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     double xr[kB][E];
     bool ok = true;
     for (int64_t b = 0; ok && b < nfull; ++b) {
+        PSGD_STAMP(const uint64_t st_w = __builtin_amdgcn_s_memtime();)
         ok = wait_rows((b + 1) * kB);
+        PSGD_STAMP(st_rd += __builtin_amdgcn_s_memtime() - st_w;)
         if (!ok) break;
         const char* base = ring + rs * ROW_BYTES;
         if constexpr (KEEP) load_rows(Full{}, xr, base, kB);
+        load_raw(Full{}, base, kB);
         ok = block(Full{}, xr, b, kB, base);
     }
     if (ok && ntail > 0 && wait_rows(n)) {
         const char* base = ring + rs * ROW_BYTES;
         if constexpr (KEEP) load_rows(Tail{}, xr, base, ntail);
+        load_raw(Tail{}, base, ntail);
         block(Tail{}, xr, nfull, ntail, base);
     }
     // a wave that stopped early leaves the others blocked on it: wake them
     __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    PSGD_STAMP(if (L.stamps && lane == 0) {
+        unsigned long long* o = L.stamps + (size_t)chain * 16;
+        o[0] = __builtin_amdgcn_s_memtime() - st_begin; o[1] = st_rd; o[2] = st_gr;
+        o[3] = st_p; o[12 + 2] = st_rec; o[12 + 3] = st_upd;
+    })
     loss_sum = wave_sum(loss_sum);   // the 8 loss lanes' partials
 
     // regVal of the chain's last update (PSGD.scala:257; 0.0 if no sample, :247)
@@ -524,6 +589,7 @@ static int launch_block64(const ChainLaunch& L, const KParams& kp, bool full, si
     return (int)hipGetLastError();
 }
 
+#ifndef PSGD_NO_DISPATCH
 template <typename S, int GRAD, int UPD>
 static int block64_nv(const ChainLaunch& L, const KParams& kp, int64_t min_ld, int64_t max_ld,
                       size_t lds, hipStream_t st, int* variant) {
@@ -577,5 +643,7 @@ int launch_block64_chains(const ChainLaunch& L, const KParams& kp, int storage, 
         return block64_grad<float>(L, kp, gradient, updater, min_ld, max_ld, lds, stream, kernel_variant);
     return block64_grad<double>(L, kp, gradient, updater, min_ld, max_ld, lds, stream, kernel_variant);
 }
+
+#endif  // PSGD_NO_DISPATCH
 
 }  // namespace psgd

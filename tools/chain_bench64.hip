@@ -1,0 +1,117 @@
+// chain_bench64.hip -- diagnostic: the fp64 blocked chain kernel (psgd_block64.hip, compiled here
+// with -DPSGD_STAMPS) on f32 rows of the bench workload's shape, per-wave s_memtime counters:
+//   chain wave: total, waiting for rows, waiting for the Gram triangle
+//   loader:     total, blocked on a full ring, in its vmcnt wait
+//   Gram waves: total, waiting for rows
+// Usage: chain_bench <rows per chain> <chains> <d> <grad 0|1|2> <upd 0|1>
+#define PSGD_STAMPS 1
+#define PSGD_NO_DISPATCH 1
+#include "../spark-parallelized-sgd_amd/csrc/psgd_block64.hip"
+// the row-loss kernel lives in psgd_kernels.hip; the diagnostic times the chain only
+int psgd::launch_logistic_loss64(const psgd::ChainLaunch&, int, hipStream_t) { return 0; }
+
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <vector>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
+
+__global__ void fill(float* x, size_t n, unsigned seed) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        unsigned h = (unsigned)i * 2654435761u ^ seed;
+        h ^= h >> 15; h *= 2246822519u; h ^= h >> 13;
+        x[i] = (float)((int)(h & 0xffff) - 32768) / 32768.0f;
+    }
+}
+__global__ void fill_d(double* x, size_t n, double v) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        x[i] = v;
+}
+
+// f32 rows, f64 compute (d = 256 / 512 / 1024: NV = 1 / 2 / 4, full rows)
+static int launch(const psgd::ChainLaunch& L, const psgd::KParams& kp, int grad, int upd, int d) {
+    const size_t lds = 160 * 1024 - 512;
+#define NVCASE(G, U)                                                                              \
+    if (grad == G && upd == U) {                                                                  \
+        if (d == 256) return psgd::launch_block64<float, G, U, 1>(L, kp, true, lds, 0);             \
+        if (d == 512) return psgd::launch_block64<float, G, U, 2>(L, kp, true, lds, 0);             \
+        if (d == 1024) return psgd::launch_block64<float, G, U, 4>(L, kp, true, lds, 0);            \
+    }
+    NVCASE(0, 0) NVCASE(1, 0) NVCASE(0, 1) NVCASE(1, 1)
+#undef NVCASE
+    return -3;
+}
+
+int main(int argc, char** argv) {
+    const int64_t rows = argc > 1 ? atoll(argv[1]) : 39062;
+    const int P = argc > 2 ? atoi(argv[2]) : 256;
+    const int d = argc > 3 ? atoi(argv[3]) : 512;
+    const int grad = argc > 4 ? atoi(argv[4]) : 1;
+    const int upd = argc > 5 ? atoi(argv[5]) : 0;
+    const size_t nx = (size_t)rows * P * d;
+    float* X; double *y, *steps, *w_in, *w_out, *rv, *loss, *cnt_d; int64_t* cnt; int* wd;
+    unsigned long long* stamps;
+    CK(hipMalloc(&X, nx * 4));
+    hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, X, nx, 12345u);
+    CK(hipMalloc(&y, rows * P * 8)); hipLaunchKernelGGL(fill_d, dim3(1024), dim3(256), 0, 0, y, (size_t)rows * P, 0.5);
+    CK(hipMalloc(&steps, rows * 8)); hipLaunchKernelGGL(fill_d, dim3(1024), dim3(256), 0, 0, steps, (size_t)rows, 1e-3);
+    CK(hipMalloc(&w_in, d * 8)); CK(hipMemset(w_in, 0, d * 8));
+    CK(hipMalloc(&w_out, (size_t)P * d * 8));
+    CK(hipMalloc(&rv, P * 8)); CK(hipMalloc(&loss, P * 8)); CK(hipMalloc(&cnt_d, P * 8)); CK(hipMalloc(&cnt, P * 8));
+    CK(hipMalloc(&wd, 16)); CK(hipMemset(wd, 0, 16));
+    CK(hipMalloc(&stamps, (size_t)P * 16 * 8)); CK(hipMemset(stamps, 0, (size_t)P * 16 * 8));
+    std::vector<psgd::ChainDesc> h(P);
+    for (int p = 0; p < P; ++p) {
+        h[p] = psgd::ChainDesc{};
+        h[p].x = X + (size_t)p * rows * d;
+        h[p].y = y + (size_t)p * rows;
+        h[p].n_rows = rows;
+        h[p].ld = d;
+    }
+    psgd::ChainDesc* dd;
+    CK(hipMalloc(&dd, P * sizeof(psgd::ChainDesc)));
+    CK(hipMemcpy(dd, h.data(), P * sizeof(psgd::ChainDesc), hipMemcpyHostToDevice));
+    psgd::ChainLaunch L{};
+    L.descs = dd; L.w_in = w_in; L.w_out = w_out; L.rv = rv; L.loss = loss; L.cnt_d = cnt_d;
+    L.cnt = cnt; L.steps = steps; L.watchdog = wd; L.stamps = stamps;
+    double* zbuf;
+    CK(hipMalloc(&zbuf, (size_t)rows * P * 8));
+    L.zbuf64 = zbuf; L.zstride = rows;
+    psgd::KParams kp{};
+    kp.reg = 0.01; kp.d = d; kp.n_chains = P;
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+    int variant = 0;
+    float best = 1e30f;
+    for (int it = 0; it < 4; ++it) {
+        CK(hipEventRecord(a));
+        int e = launch(L, kp, grad, upd, d);
+        variant = 500 + d / 256;
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        if (e) { fprintf(stderr, "launch failed %d\n", e); return 1; }
+        float ms; CK(hipEventElapsedTime(&ms, a, b));
+        if (it > 0) best = std::min(best, ms);
+    }
+    int w = 0;
+    CK(hipMemcpy(&w, wd, 4, hipMemcpyDeviceToHost));
+    std::vector<unsigned long long> st((size_t)P * 16);
+    CK(hipMemcpy(st.data(), stamps, st.size() * 8, hipMemcpyDeviceToHost));
+    const double bytes = (double)rows * P * (d + 1) * 4;
+    printf("variant %d  %.3f ms  %.1f GB/s  %.1f ns/row  watchdog=%d\n", variant, best, bytes / best / 1e6,
+           best * 1e6 / rows, w);
+    const char* names[16] = {"chain.total", "chain.wait_rows", "chain.wait_gram", "chain.p+reduce",
+                             "loader.total", "loader.ring_full", "loader.vmcnt", "-",
+                             "gram0.total", "gram0.wait_rows", "-", "-",
+                             "gram1.total", "gram1.wait_rows", "chain.recurrence", "chain.loss+update"};
+    for (int k = 0; k < 16; ++k) {
+        if (names[k][0] == '-') continue;
+        std::vector<double> v(P);
+        for (int p = 0; p < P; ++p) v[p] = (double)st[(size_t)p * 16 + k] / rows;
+        std::sort(v.begin(), v.end());
+        printf("  %-18s cycles/row  median %8.1f  min %8.1f  max %8.1f\n", names[k], v[P / 2], v[0], v[P - 1]);
+    }
+    return 0;
+}
