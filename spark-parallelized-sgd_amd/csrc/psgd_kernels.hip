@@ -200,7 +200,11 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, Ri
         const bool first = t == 0;
         const T iter = T(t + 1);
         T al = T(0);
-        if constexpr (UPD == U_ADAM) al = -(s / (T(1) - m_pow(T(kp.beta), iter)));
+        if constexpr (UPD == U_ADAM) {
+            // fp32 mode: beta^iter by the hardware log2 / exp2, as r^iter below
+            if constexpr (sizeof(T) == 4) al = -(s / (T(1) - pow_fast(T(kp.beta), iter)));
+            else al = -(s / (T(1) - m_pow(T(kp.beta), iter)));
+        }
 #pragma unroll
         for (int e = 0; e < E2; ++e) {
             const T2 old = w[e];
@@ -226,10 +230,19 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, Ri
                 ub[e] = r;
                 // fp32 mode: r^iter = exp2(iter * log2 r) (v_log_f32 / v_exp_f32; r = 0 gives 0,
                 // r > 1 overflows to inf and fix1 to NaN, as pow does)
-                const T fx = m_sqrt(T(1) - pow_fast(r.x, iter)) + T(kp.eps);
-                const T fy = m_sqrt(T(1) - pow_fast(r.y, iter)) + T(kp.eps);
-                nw.x = old.x + al * (v.x / fx);
-                nw.y = old.y + al * (v.y / fy);
+                // and v / fix1 as v * rcp(fix1), sqrt by v_sqrt_f32 (~1 ulp each; a negative
+                // 1 - r^iter still gives NaN)
+                if constexpr (sizeof(T) == 4) {
+                    const T fx = __builtin_amdgcn_sqrtf(T(1) - pow_fast(r.x, iter)) + T(kp.eps);
+                    const T fy = __builtin_amdgcn_sqrtf(T(1) - pow_fast(r.y, iter)) + T(kp.eps);
+                    nw.x = old.x + al * (v.x * __builtin_amdgcn_rcpf(fx));
+                    nw.y = old.y + al * (v.y * __builtin_amdgcn_rcpf(fy));
+                } else {
+                    const T fx = m_sqrt(T(1) - m_pow(r.x, iter)) + T(kp.eps);
+                    const T fy = m_sqrt(T(1) - m_pow(r.y, iter)) + T(kp.eps);
+                    nw.x = old.x + al * (v.x / fx);
+                    nw.y = old.y + al * (v.y / fy);
+                }
             } else if constexpr (UPD == U_SQUARED_L2) {
                 const T c = T(1) - s * T(kp.reg);
                 nw = old * c;                       // brzWeights :*= (1 - s*lambda)
