@@ -156,14 +156,28 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, Ri
         const T s = T(sb[p]);
         const T2* x = xb[p];
 
-        // dot(data, weights)
-        T2 acc0 = T2{T(0), T(0)}, acc1 = T2{T(0), T(0)};
+        // dot(data, weights): two packed partial sums; four in the fp32 mode (shorter dependent
+        // chains: the next sample's dot waits on this sample's updates)
+        T2 acc;
+        if constexpr (sizeof(T) == 4) {
+            T2 d0 = T2{T(0), T(0)}, d1 = T2{T(0), T(0)}, d2 = T2{T(0), T(0)}, d3 = T2{T(0), T(0)};
 #pragma unroll
-        for (int e = 0; e < E2; e += 2) {
-            acc0 = __builtin_elementwise_fma(x[e], w[e], acc0);
-            if (e + 1 < E2) acc1 = __builtin_elementwise_fma(x[e + 1], w[e + 1], acc1);
+            for (int e = 0; e < E2; e += 4) {
+                d0 = __builtin_elementwise_fma(x[e], w[e], d0);
+                if (e + 1 < E2) d1 = __builtin_elementwise_fma(x[e + 1], w[e + 1], d1);
+                if (e + 2 < E2) d2 = __builtin_elementwise_fma(x[e + 2], w[e + 2], d2);
+                if (e + 3 < E2) d3 = __builtin_elementwise_fma(x[e + 3], w[e + 3], d3);
+            }
+            acc = (d0 + d1) + (d2 + d3);
+        } else {
+            T2 acc0 = T2{T(0), T(0)}, acc1 = T2{T(0), T(0)};
+#pragma unroll
+            for (int e = 0; e < E2; e += 2) {
+                acc0 = __builtin_elementwise_fma(x[e], w[e], acc0);
+                if (e + 1 < E2) acc1 = __builtin_elementwise_fma(x[e + 1], w[e + 1], acc1);
+            }
+            acc = acc0 + acc1;
         }
-        const T2 acc = acc0 + acc1;
         const T z = wave_sum_uniform(acc.x + acc.y);
         if ((t & 1) == 1 || t + 1 == n) {
             // rows <= t have been read into registers: hand their slots back to the loader
