@@ -37,6 +37,7 @@
 
 #include <type_traits>
 
+
 namespace psgd {
 
 namespace {
@@ -146,9 +147,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     constexpr int VEC = Vec16<S>::N;
     constexpr int E = NV * VEC;            // features per lane
     constexpr int ROW_BYTES = NV * 1024;
-    constexpr bool KEEP = E <= 8;          // the chain wave keeps a block's rows in registers
-    // f32 rows of up to 16 features per lane: kept in registers as stored (128 VGPRs) and
-    // converted where used, so a block's rows leave LDS once, in one batch
+    // f64 rows of up to 8 features per lane: kept in registers as doubles
+    constexpr bool KEEP = E <= 8 && !std::is_same<S, float>::value;
+    // f32 rows of up to 16 features per lane: kept in registers as stored (up to 128 VGPRs) and
+    // converted where used, so a block's rows leave LDS once, in one batch (also at NV <= 2,
+    // where converted doubles would fit: half the registers, measured 15-26 % faster at d = 512)
     constexpr bool RAW = !KEEP && std::is_same<S, float>::value && E <= 16;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // LDS: [RingHeader 16 B][GramHeader64 16 B][meta ring MB x 256 B][Gram ring GS x 512 B]

@@ -435,13 +435,14 @@ def test_libsvm_file_to_chains(pkg, oracle, tmp_path):
     assert_close(h, hr, what="loss")
 
 
-@pytest.mark.parametrize("d", [700, 1024])
+@pytest.mark.parametrize("d", [100, 300, 700, 1024])
 @pytest.mark.parametrize("grad", ["least_squares", "logistic", "hinge"])
 @pytest.mark.parametrize("upd", ["simple", "squared_l2"])
 def test_fp64_block_f32_rows_in_registers(pkg, oracle, d, grad, upd):
-    """chain_block64 at NV = 4 on f32 rows (the c3 fp64 instance): the block's rows are held in
-    registers as stored and converted where used. d = 700 exercises the zero-masked row end,
-    903-row partitions a ragged last block; 1e-9 and exact counts against the oracle."""
+    """chain_block64 on f32 rows (NV = 1, 2, 4; the c2 / c3 fp64 instances): the block's rows are
+    held in registers as stored and converted where used. d = 100 / 300 / 700 exercise the
+    zero-masked row end, 903-row partitions a ragged last block; 1e-9 and exact counts against
+    the oracle."""
     rng = np.random.default_rng(d + len(grad) * 3 + len(upd))
     n, P = 2709, 3
     X, y = synth(rng, n, d, grad, np.float32)
@@ -452,7 +453,10 @@ def test_fp64_block_f32_rows_in_registers(pkg, oracle, d, grad, upd):
     U = {"simple": pkg.SimpleSGDUpdater, "squared_l2": pkg.SquaredL2SGDUpdater}
     w, h, counts = pkg.runParallelizedSGD(data, G[grad](), U[upd](), step, 3, 0.05, 1.0, np.zeros(d), 0.0,
                                           return_chain_counts=True)
-    assert pkg.optimization.get_context(0).last_kernel() == 504
+    nv = 1
+    while nv * 256 < d:
+        nv *= 2
+    assert pkg.optimization.get_context(0).last_kernel() == 500 + nv
     wr, hr, cr = oracle.run(oracle.Matrix(y, X.astype(np.float64)), offs, grad, upd, step, 3, 0.05,
                             np.zeros(d), tol=0.0, n_threads=8)
     assert [list(c) for c in counts] == [list(c) for c in cr[: len(counts)]]
