@@ -35,15 +35,18 @@ WORKLOADS = {
            "Hinge-loss linear SVM, sparse CSR rcv1-like (47,236 features, 94 nnz/row = 0.2%)"),
     "c5": ("logistic", 125_000_000, 1 << 22, 1024, 0.5, "f32",
            "L2 logistic regression, sparse 2^22 features (HBM-resident weights), 1B rows over 8 GPUs: "
-           "per-GPU shard 125M rows, 1024 of 8192 chains, lambda 1e-6"),
+           "1024 of 8192 chains per GPU, lambda 1e-6"),
 }
 CSR_NNZ = {"c4": 94, "c5": 100}  # nonzeros per row (c4: rcv1's mean; c5: SURVEY §8d)
 REG = {"c5": 1e-6}                # SquaredL2 regParam (c5); others: Simple updater
 # secondary lines: rows per GPU (0 = the workload's own; c5's full 125M-row shard takes minutes)
 SECONDARY_ROWS = {"c5": 20_000_000}
+# secondary specs are workload[:compute[:updater[:storage]]]; c3 with f64 storage is the
+# reference's own Double rows (8,200 B per sample)
 # (AdaGrad / Adam on the logistic c3 shard: the reference's Adam, r^iter in fix1 (UPD.scala:262),
 # turns NaN once the squared-gradient average r exceeds 1, which least squares at c2 reaches)
-DEFAULT_SECONDARY = "c3:f64,c3:f32,c2:f64,c1:f64,c4:f32,c5:f32,c3:f32:adagrad,c3:f32:adam"
+DEFAULT_SECONDARY = ("c3:f64,c3:f64::f64,c3:f32,c2:f64,c1:f64,c4:f32,c5:f32,"
+                     "c3:f32:adagrad,c3:f32:adam")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
@@ -55,14 +58,18 @@ def pmc_traffic(workload, grad, variant, storage, rows, compute="f32", updater="
     import glob
     files = glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_pmc.json")) + \
         glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_*_pmc.json"))
-    if not files or not (300 <= variant < 700):
+    if not files or not (300 <= variant < 800):
         return None, None
+    waves = 0
     g = {"logistic": 0, "least_squares": 1, "hinge": 2}[grad]
     u = {"simple": 0, "squared_l2": 1}.get(updater)
     if u is None:
         return None, None
     sname = "float" if storage == "f32" else "double"
-    if variant >= 600:
+    if variant >= 700:
+        prefix = f"psgd::chain_block64<{sname}, {g}, {u}, {variant % 10}, "
+        waves = 1 + (variant - 700) // 10
+    elif variant >= 600:
         prefix = f"psgd::chain_sparse_lds<{sname}, {g}, {u},"
     elif variant >= 500:
         prefix = f"psgd::chain_block64<{sname}, {g}, {u}, {variant - 500},"
@@ -77,6 +84,8 @@ def pmc_traffic(workload, grad, variant, storage, rows, compute="f32", updater="
         with open(path) as f:
             summ = json.load(f)
         for name, e in summ.get("kernels", {}).items():
+            if waves and not name.rstrip(">").endswith(f", {waves}"):
+                continue   # chain_block64<S, GRAD, UPD, NV, FULL, H>: the same number of chain waves
             if name.startswith(prefix) and "hbm_bytes" in e:
                 # the summary's launch may have processed a different row count (--rows): per row
                 per_row = e["hbm_bytes"] / max(summ.get("rows_per_launch") or rows, 1)
@@ -85,10 +94,12 @@ def pmc_traffic(workload, grad, variant, storage, rows, compute="f32", updater="
 
 
 def kernel_name(variant):
+    if 700 <= variant < 800:
+        waves = 1 + (variant - 700) // 10
+        return (f"chain_block64 (NV={variant % 10}: blocked fp64 chain, 8-row Gram blocks, "
+                f"{waves} chain wave{'s' if waves > 1 else ''})")
     if 300 <= variant < 400:
         return f"chain_block (NV={variant - 300}: blocked fp32 chain, 8-row Gram blocks)"
-    if 500 <= variant < 600:
-        return f"chain_block64 (NV={variant - 500}: blocked fp64 chain, 8-row Gram blocks)"
     if 600 <= variant < 700:
         return (f"chain_sparse_lds (fp32 CSR chain, weights LDS-resident [tail past ~160 KiB: L2-resident, "
                 f"gathered {8 if variant >= 610 else 4} samples ahead with an LDS feature-tag correction])")
@@ -119,6 +130,8 @@ def parse():
     ap.add_argument("--secondary", default=DEFAULT_SECONDARY,
                     help="comma list of workload[:compute[:updater]] measured after the headline (1 GPU only; '' = none)")
     ap.add_argument("--updater", default="", help="another SGDUpdater for the headline workload (experiments)")
+    ap.add_argument("--storage", default="", choices=["", "f32", "f64"],
+                    help="row storage dtype of the headline workload (default: the workload's own)")
     ap.add_argument("--prewarm-s", type=float, default=1.0,
                     help="untimed epochs for this long before the warmup steps (GPU clock ramp)")
     return ap.parse_args()
@@ -176,14 +189,27 @@ def make_csr_shard(torch, dev, n, d, P, grad, dtype, seed, nnz):
     return row_ptr, col.reshape(-1), val.reshape(-1), y, offs
 
 
+def host_cpus():
+    """CPUs this process may run on: its affinity set, capped by a cgroup-v2 CPU quota when one
+    is set (a container's share of the host), so the baseline's threads all run at once."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def cpu_baseline(grad, d, P, step, budget_s, seed=7, csr_nnz=0):
     """Time the CPU restatement of the reference (oracle/, one thread per partition, all host
     cores) on a bounded sample of the same workload: the first m rows of every partition."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    cores = len(os.sched_getaffinity(0))
-    cores = min(cores, 16, P)
+    cores = min(host_cpus(), P)
     rng = np.random.default_rng(seed)
 
     def sample(m):
@@ -221,6 +247,7 @@ def cpu_baseline(grad, d, P, step, budget_s, seed=7, csr_nnz=0):
         if dt >= budget_s:
             break
     return {"value": total / dt, "unit": "samples/s", "cores": cores, "kind": "port",
+            "host_cpus": host_cpus(), "nproc": os.cpu_count(),
             "sample": f"oracle/psgd_oracle.c (fp64 CPU restatement of ParallelizedSGD.scala:243-270 "
                       f"incl. per-sample isConverged), {P} partitions x {m} "
                       f"{'CSR (%d nnz) ' % csr_nnz if csr_nnz else ''}rows, d={d}, "
@@ -228,11 +255,16 @@ def cpu_baseline(grad, d, P, step, budget_s, seed=7, csr_nnz=0):
 
 
 def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, rows, fraction,
-                 steps, warmup, prewarm_s, features=0, chains=0, updater=""):
+                 steps, warmup, prewarm_s, features=0, chains=0, updater="", storage=""):
     """One workload: synthetic shard in HBM, prewarm, W warmup steps, K timed steps (barrier +
     synchronize on both sides, max over ranks). Returns the measurement as a dict."""
     import numpy as np
     grad, n, d, P, step, sdt, cfg_name = WORKLOADS[workload]
+    if storage and storage != sdt:
+        sdt = storage
+        cfg_name += f" [{sdt} storage" + (": the reference's Double rows]" if sdt == "f64" else "]")
+    if rows and rows != n:
+        cfg_name += f" [this run: {rows:,} rows per GPU of the {n:,}-row shard]"
     if rows:
         n = rows
     if features:
@@ -414,7 +446,7 @@ def main():
 
     res = run_workload(torch, dist, pkg, dev, rank, world, local, args.workload, args.compute,
                        args.rows, args.fraction, args.steps, args.warmup, args.prewarm_s, args.features,
-                       args.chains, args.updater)
+                       args.chains, args.updater, args.storage)
     grad, d, P, step, csr = res.pop("_meta")
     res.pop("loss")
     out = {
@@ -434,19 +466,29 @@ def main():
     if secondary:
         out["secondary"] = []
     for spec in secondary:
-        wl, comp, upd = (spec.split(":") + ["", ""])[:3]
+        wl, comp, upd, sto = (spec.split(":") + ["", "", ""])[:4]
         torch.cuda.empty_cache()
         try:
             r = run_workload(torch, dist, pkg, dev, rank, world, local, wl, comp or "f32",
                              SECONDARY_ROWS.get(wl, 0), 1.0, args.steps, args.warmup,
-                             min(args.prewarm_s, 0.5), updater=upd)
+                             min(args.prewarm_s, 0.5), updater=upd, storage=sto)
         except Exception as e:   # a secondary line never hides the headline
             out["secondary"].append({"spec": spec, "error": f"{type(e).__name__}: {e}"})
             continue
         r.pop("_meta")
+        r["spec"] = spec
         r["samples_per_s"] = r.pop("value")
         r["loss"] = float(r["loss"])
         out["secondary"].append(r)
+    if secondary:
+        # the same numbers once more, compact and last on the line: a reader that keeps only
+        # the line's tail still sees every secondary measurement
+        out["secondary_summary"] = [
+            {"spec": r["spec"], "error": r["error"]} if "error" in r else
+            {"spec": r["spec"], "samples_per_s": round(r["samples_per_s"]),
+             "frac": round(r["roofline"]["frac"], 4), "kernel_ms": round(r["roofline"]["avg_kernel_ms"], 3),
+             "B_per_sample": r["roofline"]["bytes_per_sample"]}
+            for r in out["secondary"]]
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -93,11 +93,12 @@ int32_t psgd_ctx_destroy(psgd_ctx* ctx);
  * threads; their copies run concurrently). Empty partitions (n_rows == 0) must be registered
  * too: they take part in the combine with count 0 (PSGD.scala:270-276). Replaces the
  * mapPartitions closure input at PSGD.scala:243-253.
- * Ingest: pinned sources (psgd_host_alloc) are DMA'd directly and waited for; pageable ones are
- * packed through the context's pinned staging ring, the DMA of one chunk overlapping the packing
- * of the next, on a copy stream of their own. The call returns once the caller's memory has been
- * read (the last chunks may still be in flight from the library's buffers); the next epoch waits
- * for them on the device, psgd_register_wait on the host. */
+ * Ingest: pinned sources (psgd_host_alloc) are DMA'd directly; pageable ones are packed through
+ * a pinned staging ring, the DMA of one chunk overlapping the packing of the next, on a copy
+ * stream of their own. The call returns once every copy it enqueued has landed in HBM (the
+ * staging ring is drained before it goes back to the pool), so concurrent registrations from
+ * several threads overlap each other, not the caller's next statement; an epoch that starts
+ * while another thread's registration is in flight waits for it on the device. */
 int32_t psgd_register_dense(psgd_ctx* ctx, int64_t part, int64_t n_rows, int32_t d,
                             const double* labels, const void* x, int32_t dtype);
 

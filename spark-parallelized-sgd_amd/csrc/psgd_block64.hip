@@ -141,24 +141,47 @@ __device__ __forceinline__ double row_loss64(double z, double y) {
 
 }  // namespace
 
-template <typename S, int GRAD, int UPD, int NV, bool FULL>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
+// The chain waves of one chain (H = 2) exchange their partial dots through LDS once per block:
+// per block parity and chain wave, one partial per row; at the chain's end, the partial ||w||^2.
+struct XchgHeader64 {
+    unsigned xdone[2];   // blocks whose partial dots chain wave 0 / 1 has published
+    unsigned fin[2];     // chain wave 0 / 1 has published its partial ||w||^2
+};
+constexpr int kXchgDoubles = 2 * 2 * kB + 2;
+constexpr size_t kFixed64 = sizeof(RingHeader) + sizeof(GramHeader64) + sizeof(XchgHeader64) +
+                            kXchgDoubles * sizeof(double);
+static_assert(kFixed64 % 16 == 0, "the meta and row rings start 16-byte aligned");
+
+// f32 rows: a chain wave that owns at most 8 features per lane converts its share of a block to
+// doubles once (64 VGPRs of rows become 128); 0 converts at every use (dot and update).
+#ifndef PSGD_B64_CONV1
+#define PSGD_B64_CONV1 1
+#endif
+
+template <typename S, int GRAD, int UPD, int NV, bool FULL, int H>
+__global__ __launch_bounds__(64 * (3 + H)) __attribute__((amdgpu_waves_per_eu(H, H)))
+void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
     using V = typename Vec16<S>::type;
     constexpr int VEC = Vec16<S>::N;
-    constexpr int E = NV * VEC;            // features per lane
+    constexpr bool F32 = std::is_same<S, float>::value;
+    constexpr int NVH = NV / H;            // 1 KiB row slices owned by one chain wave
+    constexpr int EH = NVH * VEC;          // features per lane of one chain wave
     constexpr int ROW_BYTES = NV * 1024;
-    // f64 rows of up to 8 features per lane: kept in registers as doubles
-    constexpr bool KEEP = E <= 8 && !std::is_same<S, float>::value;
-    // f32 rows of up to 16 features per lane: kept in registers as stored (up to 128 VGPRs) and
-    // converted where used, so a block's rows leave LDS once, in one batch (also at NV <= 2,
-    // where converted doubles would fit: half the registers, measured 15-26 % faster at d = 512)
-    constexpr bool RAW = !KEEP && std::is_same<S, float>::value && E <= 16;
+    static_assert(H == 1 || H == 2, "one or two chain waves");
+    static_assert(NV % H == 0, "the chain waves split the row slices evenly");
+    static_assert(EH <= (F32 ? 16 : 8), "a chain wave keeps its share of a block's rows in registers");
+    constexpr bool CONV1 = F32 && H == 2 && EH <= 8 && PSGD_B64_CONV1;
+    // wave roles: chain waves 0 .. H-1, Gram waves 2 and 3, the loader (H = 2: wave 4, which
+    // shares the first chain wave's SIMD; it mostly sleeps on the ring)
+    constexpr int kLoaderWave = H == 1 ? 1 : 4;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    // LDS: [RingHeader 16 B][GramHeader64 16 B][meta ring MB x 256 B][Gram ring GS x 512 B]
-    //      [row ring R x ROW_BYTES]
+    // LDS: [RingHeader 16 B][GramHeader64 16 B][XchgHeader64 16 B][exchange 34 doubles]
+    //      [meta ring MB x 256 B][Gram ring GS x 512 B][row ring R x ROW_BYTES]
     RingHeader* hdr = reinterpret_cast<RingHeader*>(smem);
     GramHeader64* ghdr = reinterpret_cast<GramHeader64*>(smem + sizeof(RingHeader));
-    char* meta_ring = smem + sizeof(RingHeader) + sizeof(GramHeader64);
+    XchgHeader64* xhdr = reinterpret_cast<XchgHeader64*>(smem + sizeof(RingHeader) + sizeof(GramHeader64));
+    double* xchg = reinterpret_cast<double*>(smem + sizeof(RingHeader) + sizeof(GramHeader64) + sizeof(XchgHeader64));
+    char* meta_ring = smem + kFixed64;
     double* gring = reinterpret_cast<double*>(meta_ring + geom.meta_blocks * kMetaBlockBytes);
     const int GS = geom.gslots;
     char* ring = reinterpret_cast<char*>(gring + GS * kB * kB);
@@ -177,17 +200,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         hdr->ready = 0;
         hdr->consumed = 0;
         hdr->stop = 0;
+        hdr->consumed1 = 0;
         ghdr->gdone[0] = 0;
         ghdr->gdone[1] = 0;
         ghdr->gread[0] = 0;
         ghdr->gread[1] = 0;
+        xhdr->xdone[0] = 0;
+        xhdr->xdone[1] = 0;
+        xhdr->fin[0] = 0;
+        xhdr->fin[1] = 0;
     }
     // entries on and above the diagonal stay zero (the Gram waves write only i < k)
     for (int i = threadIdx.x; i < GS * kB * kB; i += blockDim.x) gring[i] = 0.0;
     __syncthreads();
 
-    if (wave == 1) {
-        ring_loader<S, NV, FULL, kB, kB>(L, dsc, hdr, meta_ring, ring, geom, lane, ghdr->gread);
+    if (wave == kLoaderWave) {
+        ring_loader<S, NV, FULL, kB, kB, H>(L, dsc, hdr, meta_ring, ring, geom, lane, ghdr->gread);
         return;
     }
 
@@ -204,7 +232,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                 __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 return false;
             }
-            if (code != 2) __builtin_amdgcn_s_sleep(1);   // the chain wave polls without sleeping
+            if (code != 2) __builtin_amdgcn_s_sleep(1);   // the chain waves poll without sleeping
         }
     };
     // One 16-byte vector of a row slot as doubles, zero past the row end (stale LDS bytes).
@@ -284,16 +312,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         return;
     }
 
-    // ---------------- chain wave ----------------
-    double w[E];
+    // ---------------- chain waves ----------------
+    // Chain wave h owns the row slices [h*NVH, (h+1)*NVH): lane l holds features
+    // ((h*NVH + u)*64 + l)*VEC .. +VEC-1 of W, u < NVH. With H = 2 each wave takes the partial
+    // dots of a block over its features; the two partials of row k are added as p0 + p1 in both
+    // waves, so both run the identical scalar recurrence and update their own features.
+    const int h = wave;
+    const bool lead = h == 0;                 // the loss terms, count and regVal
+    double w[EH];
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-        const int base = (v * 64 + lane) * VEC;
+    for (int u = 0; u < NVH; ++u) {
+        const int base = ((h * NVH + u) * 64 + lane) * VEC;
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
             const int f = base + k;
             const double wv = as_global(L.w_in)[f < d ? f : 0];
-            w[v * VEC + k] = f < d ? wv : 0.0;
+            w[u * VEC + k] = f < d ? wv : 0.0;
         }
     }
     const int krow = ((lane >> 5) & 1) | (((lane >> 4) & 1) << 1) | (((lane >> 3) & 1) << 2);
@@ -302,6 +336,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // the chain (log1pExp is a second exp and a log1p; off the sequential wave)
     constexpr bool LOSS_EXT = GRAD == G_LOGISTIC;
     gmut<double> zout = as_global_mut(L.zbuf64 + (LOSS_EXT ? (int64_t)chain * L.zstride : 0));
+    unsigned* const my_consumed = (H == 2 && h == 1) ? &hdr->consumed1 : &hdr->consumed;
     const double lam = kp.reg;
     double loss_sum = 0.0;
     int64_t count = 0;
@@ -309,86 +344,66 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     int rs = 0, gs = 0, ms = 0;      // ring slot, Gram slot and meta block of the current block
     const int64_t nfull = n / kB;
     const int ntail = (int)(n - nfull * kB);
-    PSGD_STAMP(const uint64_t st_begin = __builtin_amdgcn_s_memtime(); uint64_t st_rd = 0, st_gr = 0, st_p = 0, st_rec = 0, st_upd = 0;)
+    PSGD_STAMP(const uint64_t st_begin = __builtin_amdgcn_s_memtime(); uint64_t st_rd = 0, st_gr = 0, st_p = 0, st_rec = 0, st_upd = 0, st_x = 0;)
 
     auto wait_rows = [&](int64_t rows) __attribute__((always_inline)) -> bool {
         return wait_ready(ready, rows, 2);
     };
-    // A block's rows from the ring into registers; rows >= kk (a tail block) read as zero.
-    auto load_rows = [&](auto tail_c, double (&xr)[kB][E], const char* base, int kk) __attribute__((always_inline)) {
+    // This wave's share of a block's rows, from the ring into registers (as stored, or as
+    // doubles with CONV1); rows >= kk (a tail block) are zero.
+    V xraw[kB][CONV1 ? 1 : NVH];
+    double xcv[CONV1 ? kB : 1][CONV1 ? EH : 1];
+    auto load_rows = [&](auto tail_c, const char* base, int kk) __attribute__((always_inline)) {
         constexpr bool TAIL = decltype(tail_c)::value;
 #pragma unroll
         for (int k = 0; k < kB; ++k) {
 #pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                double xv[VEC];
-                read_vec(base + k * ROW_BYTES, v, xv);
-#pragma unroll
-                for (int h = 0; h < VEC; ++h) xr[k][v * VEC + h] = (TAIL && k >= kk) ? 0.0 : xv[h];
-            }
-        }
-    };
-
-    V xraw[kB][RAW ? NV : 1];
-    // A block's rows from the ring into registers as stored; rows >= kk (a tail block) are zero.
-    auto load_raw = [&](auto tail_c, const char* base, int kk) __attribute__((always_inline)) {
-        constexpr bool TAIL = decltype(tail_c)::value;
-        if constexpr (RAW) {
-#pragma unroll
-            for (int k = 0; k < kB; ++k) {
-#pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    V xv = *reinterpret_cast<const V*>(base + k * ROW_BYTES + v * 1024 + lane * 16);
-                    if constexpr (!FULL) {
-                        if ((v * 64 + lane) * VEC >= dsc.ld) xv = V(0);
-                    }
-                    xraw[k][v] = (TAIL && k >= kk) ? V(0) : xv;
+            for (int u = 0; u < NVH; ++u) {
+                const int v = h * NVH + u;
+                V xv = *reinterpret_cast<const V*>(base + k * ROW_BYTES + v * 1024 + lane * 16);
+                if constexpr (!FULL) {
+                    if ((v * 64 + lane) * VEC >= dsc.ld) xv = V(0);
                 }
+                if (TAIL && k >= kk) xv = V(0);
+                if constexpr (CONV1) unpack<S, double>(xv, &xcv[k][u * VEC]);
+                else xraw[k][u] = xv;
             }
         }
     };
-    // One block: rows in xr (KEEP), in xraw (RAW) or in the ring at `base`; kk rows (kB unless TAIL).
-    auto block = [&](auto tail_c, double (&xr)[kB][E], int64_t b, int kk, const char* base)
-                     __attribute__((always_inline)) -> bool {
+    // VEC doubles of row k, slice u
+    auto xrow = [&](int k, int u, double* out) __attribute__((always_inline)) {
+        if constexpr (CONV1) {
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) out[q] = xcv[k][u * VEC + q];
+        } else {
+            unpack<S, double>(xraw[k][u], out);
+        }
+    };
+    // One block of kk rows (kB unless TAIL), rows in registers.
+    auto block = [&](auto tail_c, int64_t b, int kk) __attribute__((always_inline)) -> bool {
         constexpr bool TAIL = decltype(tail_c)::value;
         const int64_t t0 = b * kB;
         // this lane's row: label and stepSize/sqrt(j)
         const f64x2 meta = *reinterpret_cast<const f64x2*>(
             meta_ring + ms * kMetaBlockBytes + ((int)(b & 1) * kB + krow) * 16);
-        if constexpr (KEEP || RAW) {
-            // rows are in registers (the Gram and meta slots are reused only after the next
-            // block is handed back): free the ring slots (the loader also waits for the Gram)
-            __hip_atomic_store(&hdr->consumed, (unsigned)(t0 + kk), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
+        // the rows are in registers (the Gram and meta slots are reused only after the next
+        // block is handed back): free the ring slots (the loader also waits for the Gram)
+        __hip_atomic_store(my_consumed, (unsigned)(t0 + kk), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         // flags this block tests, read now so that their LDS round trip lands under the dots
         const unsigned gpre = __hip_atomic_load(&ghdr->gdone[b & 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const unsigned rpre = __hip_atomic_load(&hdr->ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         PSGD_STAMP(const uint64_t st_a = __builtin_amdgcn_s_memtime();)
-        // p_k = x_k . W
+        // p_k = x_k . W over this wave's features
         double pk[kB];
 #pragma unroll
         for (int k = 0; k < kB; ++k) {
             double a = 0.0;
-            if constexpr (KEEP) {
 #pragma unroll
-                for (int e = 0; e < E; ++e) a = __builtin_fma(xr[k][e], w[e], a);
-            } else if constexpr (RAW) {
+            for (int u = 0; u < NVH; ++u) {
+                double xv[VEC];
+                xrow(k, u, xv);
 #pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    double xv[VEC];
-                    unpack<S, double>(xraw[k][v], xv);
-#pragma unroll
-                    for (int h = 0; h < VEC; ++h) a = __builtin_fma(xv[h], w[v * VEC + h], a);
-                }
-            } else {
-#pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    double xv[VEC];
-                    read_vec(base + k * ROW_BYTES, v, xv);
-#pragma unroll
-                    for (int h = 0; h < VEC; ++h) a = __builtin_fma(xv[h], w[v * VEC + h], a);
-                }
+                for (int q = 0; q < VEC; ++q) a = __builtin_fma(xv[q], w[u * VEC + q], a);
             }
             pk[k] = a;
         }
@@ -396,6 +411,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         const double nsv = -sv;
         const double alpha = 1.0 - sv * lam;      // SquaredL2 shrink of this lane's row (UPD:169)
         double z = reduce8d(pk, lane);
+        if constexpr (H == 2) {
+            // publish this wave's partial of every row (one lane per row), then the block count
+            double* xs = xchg + ((int)(b & 1) * 2 + h) * kB;
+            if (loss_lane) xs[krow] = z;
+            asm volatile("s_waitcnt lgkmcnt(0)" : : : "memory");
+            __hip_atomic_store(&xhdr->xdone[h], (unsigned)(b + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
         PSGD_STAMP(const uint64_t st_b = __builtin_amdgcn_s_memtime(); st_p += st_b - st_a;)
         // the block's Gram triangle (Gram wave b&1 publishes its blocks in order)
         {
@@ -421,6 +443,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             G[2 * q] = g2.x;
             G[2 * q + 1] = g2.y;
         }
+        if constexpr (H == 2) {
+            // the other chain wave's partial of this lane's row: z = p0 + p1 in both waves
+            const unsigned need = (unsigned)(b + 1);
+            unsigned* xo = &xhdr->xdone[h ^ 1];
+            if (__hip_atomic_load(xo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+                const uint64_t tw = __builtin_amdgcn_s_memrealtime();
+                for (;;) {
+                    if (__hip_atomic_load(xo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= need) break;
+                    if (__hip_atomic_load(&hdr->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                        if (__hip_atomic_load(xo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= need) break;
+                        return false;
+                    }
+                    if (__builtin_amdgcn_s_memrealtime() - tw > kWatchdogTicks) {
+                        __hip_atomic_fetch_or(L.watchdog, 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        return false;
+                    }
+                }
+            }
+            asm volatile("" : : : "memory");   // the partial is read after its count
+            const double other = xchg[((int)(b & 1) * 2 + (h ^ 1)) * kB + krow];
+            z = h == 0 ? z + other : other + z;
+        }
+        PSGD_STAMP(const uint64_t st_xe = __builtin_amdgcn_s_memtime(); st_x += st_xe - st_g;)
 
         // the scalar recurrence: c_i from z_i, then every later row's dot moves by c_i G[k][i]
         // (SquaredL2 also shrinks the finished rows' z: zf keeps z_k for the loss)
@@ -440,54 +486,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             }
         }
         if constexpr (UPD != U_SQUARED_L2) zf = z;
-        if constexpr (LOSS_EXT) {
-            if (loss_lane && (!TAIL || krow < kk)) zout[t0 + krow] = zf;
-        } else {
-            const double l = row_loss64<GRAD>(zf, yv);
-            if (loss_lane && (!TAIL || krow < kk)) loss_sum += l;
+        if (lead) {
+            if constexpr (LOSS_EXT) {
+                if (loss_lane && (!TAIL || krow < kk)) zout[t0 + krow] = zf;
+            } else {
+                const double l = row_loss64<GRAD>(zf, yv);
+                if (loss_lane && (!TAIL || krow < kk)) loss_sum += l;
+            }
         }
         count += kk;
         if (rpre > ready) ready = rpre;
-        PSGD_STAMP(const uint64_t st_c = __builtin_amdgcn_s_memtime(); st_rec += st_c - st_g;)
+        PSGD_STAMP(const uint64_t st_c = __builtin_amdgcn_s_memtime(); st_rec += st_c - st_xe;)
 
-        // W <- a_i W + c_i x_i, i = 0..kk-1, in sample order
+        // W <- a_i W + c_i x_i, i = 0..kB-1, in sample order (a tail block's missing rows are
+        // zero with c_i = 0, a_i = 1: they leave W as it is)
 #pragma unroll
         for (int i = 0; i < kB; ++i) {
-            if constexpr (KEEP) {
 #pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    if constexpr (UPD == U_SQUARED_L2) w[e] = __builtin_fma(c[i], xr[i][e], w[e] * al[i]);
-                    else w[e] = __builtin_fma(c[i], xr[i][e], w[e]);
-                }
-            } else if constexpr (RAW) {
+            for (int u = 0; u < NVH; ++u) {
+                double xv[VEC];
+                xrow(i, u, xv);
 #pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    double xv[VEC];
-                    unpack<S, double>(xraw[i][v], xv);
-#pragma unroll
-                    for (int h = 0; h < VEC; ++h) {
-                        const int e = v * VEC + h;
-                        if constexpr (UPD == U_SQUARED_L2) w[e] = __builtin_fma(c[i], xv[h], w[e] * al[i]);
-                        else w[e] = __builtin_fma(c[i], xv[h], w[e]);
-                    }
-                }
-            } else if (!TAIL || i < kk) {
-#pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    double xv[VEC];
-                    read_vec(base + i * ROW_BYTES, v, xv);
-#pragma unroll
-                    for (int h = 0; h < VEC; ++h) {
-                        const int e = v * VEC + h;
-                        if constexpr (UPD == U_SQUARED_L2) w[e] = __builtin_fma(c[i], xv[h], w[e] * al[i]);
-                        else w[e] = __builtin_fma(c[i], xv[h], w[e]);
-                    }
+                for (int q = 0; q < VEC; ++q) {
+                    const int e = u * VEC + q;
+                    if constexpr (UPD == U_SQUARED_L2) w[e] = __builtin_fma(c[i], xv[q], w[e] * al[i]);
+                    else w[e] = __builtin_fma(c[i], xv[q], w[e]);
                 }
             }
-        }
-        if constexpr (!KEEP && !RAW) {
-            __hip_atomic_store(&hdr->consumed, (unsigned)(t0 + kk), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         PSGD_STAMP(st_upd += __builtin_amdgcn_s_memtime() - st_c;)
         rs += kB;
@@ -499,30 +524,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
     using Full = std::integral_constant<bool, false>;
     using Tail = std::integral_constant<bool, true>;
-    double xr[kB][E];
     bool ok = true;
     for (int64_t b = 0; ok && b < nfull; ++b) {
         PSGD_STAMP(const uint64_t st_w = __builtin_amdgcn_s_memtime();)
         ok = wait_rows((b + 1) * kB);
         PSGD_STAMP(st_rd += __builtin_amdgcn_s_memtime() - st_w;)
         if (!ok) break;
-        const char* base = ring + rs * ROW_BYTES;
-        if constexpr (KEEP) load_rows(Full{}, xr, base, kB);
-        load_raw(Full{}, base, kB);
-        ok = block(Full{}, xr, b, kB, base);
+        load_rows(Full{}, ring + rs * ROW_BYTES, kB);
+        ok = block(Full{}, b, kB);
     }
     if (ok && ntail > 0 && wait_rows(n)) {
-        const char* base = ring + rs * ROW_BYTES;
-        if constexpr (KEEP) load_rows(Tail{}, xr, base, ntail);
-        load_raw(Tail{}, base, ntail);
-        block(Tail{}, xr, nfull, ntail, base);
+        load_rows(Tail{}, ring + rs * ROW_BYTES, ntail);
+        block(Tail{}, nfull, ntail);
     }
     // a wave that stopped early leaves the others blocked on it: wake them
     __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    PSGD_STAMP(if (L.stamps && lane == 0) {
+    PSGD_STAMP(if (L.stamps && lead && lane == 0) {
         unsigned long long* o = L.stamps + (size_t)chain * 16;
         o[0] = __builtin_amdgcn_s_memtime() - st_begin; o[1] = st_rd; o[2] = st_gr;
-        o[3] = st_p; o[12 + 2] = st_rec; o[12 + 3] = st_upd;
+        o[3] = st_p; o[7] = st_x; o[12 + 2] = st_rec; o[12 + 3] = st_upd;
     })
     loss_sum = wave_sum(loss_sum);   // the 8 loss lanes' partials
 
@@ -531,8 +551,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if constexpr (UPD == U_SQUARED_L2) {
         double acc = 0.0;
 #pragma unroll
-        for (int e = 0; e < E; ++e) acc += w[e] * w[e];
+        for (int e = 0; e < EH; ++e) acc += w[e] * w[e];
         acc = wave_sum(acc);
+        if constexpr (H == 2) {
+            // ||w||^2 = n0 + n1 from the two chain waves' features
+            if (lane == 0) xchg[2 * 2 * kB + h] = acc;
+            asm volatile("s_waitcnt lgkmcnt(0)" : : : "memory");
+            __hip_atomic_store(&xhdr->fin[h], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (lead) {
+                const uint64_t tw = __builtin_amdgcn_s_memrealtime();
+                while (!__hip_atomic_load(&xhdr->fin[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                    if (__builtin_amdgcn_s_memrealtime() - tw > kWatchdogTicks) {
+                        __hip_atomic_fetch_or(L.watchdog, 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                }
+                asm volatile("" : : : "memory");
+                acc = acc + xchg[2 * 2 * kB + 1];
+            }
+        }
         if (count > 0) {
             const double nrm = sqrt(acc);
             rv = 0.5 * kp.reg * nrm * nrm;
@@ -541,13 +578,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
     double* wo = L.w_out + (int64_t)chain * d;
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-        const int base = (v * 64 + lane) * VEC;
+    for (int u = 0; u < NVH; ++u) {
+        const int base = ((h * NVH + u) * 64 + lane) * VEC;
 #pragma unroll
         for (int k = 0; k < VEC; ++k)
-            if (base + k < d) wo[base + k] = w[v * VEC + k];
+            if (base + k < d) wo[base + k] = w[u * VEC + k];
     }
-    if (lane == 0) {
+    if (lead && lane == 0) {
         L.rv[chain] = rv;
         if constexpr (!LOSS_EXT) L.loss[chain] = loss_sum;
         L.cnt[chain] = count;
@@ -558,32 +595,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 // ------------------------------------------------------------------------------------------
 // Launcher.
 // ------------------------------------------------------------------------------------------
-template <typename S, int GRAD, int UPD, int NV>
+template <typename S, int GRAD, int UPD, int NV, int H>
 static int launch_block64(const ChainLaunch& L, const KParams& kp, bool full, size_t lds, hipStream_t st) {
     constexpr int ROW = NV * 1024;
     const size_t budget = lds > 0 ? lds : (size_t)64 * 1024;
-    const size_t fixed = sizeof(RingHeader) + sizeof(GramHeader64);
     const int D = loader_depth<NV>();
     auto bytes_for = [&](int r) {
         const int mb = (r + kMetaRows - 1) / kMetaRows + 2;
         const int gs = r / kB + 1;
-        return fixed + (size_t)mb * kMetaBlockBytes + (size_t)gs * kB * kB * 8 + (size_t)r * ROW;
+        return kFixed64 + (size_t)mb * kMetaBlockBytes + (size_t)gs * kB * kB * 8 + (size_t)r * ROW;
     };
-    int R = (int)((budget - fixed) / ROW) / kB * kB;
+    int R = (int)((budget - kFixed64) / ROW) / kB * kB;
     while (R > 0 && bytes_for(R) > budget) R -= kB;
     if (R < 2 * kB) return (int)hipErrorInvalidValue;   // LDS budget too small for this d
     const int MB = (R + kMetaRows - 1) / kMetaRows + 2;
     const int GS = R / kB + 1;
     RingGeom g{R, MB, D, GS};
     const size_t bytes = bytes_for(R);
+    const dim3 threads(64 * (3 + H));
     if (full) {
-        auto k = chain_block64<S, GRAD, UPD, NV, true>;
+        auto k = chain_block64<S, GRAD, UPD, NV, true, H>;
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-        hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(256), bytes, st, L, kp, g);
+        hipLaunchKernelGGL(k, dim3(kp.n_chains), threads, bytes, st, L, kp, g);
     } else {
-        auto k = chain_block64<S, GRAD, UPD, NV, false>;
+        auto k = chain_block64<S, GRAD, UPD, NV, false, H>;
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-        hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(256), bytes, st, L, kp, g);
+        hipLaunchKernelGGL(k, dim3(kp.n_chains), threads, bytes, st, L, kp, g);
     }
     if constexpr (GRAD == G_LOGISTIC) {
         const int e = launch_logistic_loss64(L, kp.n_chains, st);
@@ -593,19 +630,33 @@ static int launch_block64(const ChainLaunch& L, const KParams& kp, bool full, si
 }
 
 #ifndef PSGD_NO_DISPATCH
+// Two chain waves (H = 2) from NV = 2 on; PSGD_B64_WAVES=1 keeps one where its share of a
+// block fits the registers (NV <= 4; A/B measurements). Variant 700 + 10 (H - 1) + NV.
 template <typename S, int GRAD, int UPD>
 static int block64_nv(const ChainLaunch& L, const KParams& kp, int64_t min_ld, int64_t max_ld,
                       size_t lds, hipStream_t st, int* variant) {
     constexpr int VEC = 16 / sizeof(S);
+    static const bool one_wave = [] {
+        const char* e = getenv("PSGD_B64_WAVES");
+        return e && atoi(e) == 1;
+    }();
     int nv = 1;
     while (nv * 64 * VEC < max_ld) nv *= 2;
     const bool full = min_ld >= (int64_t)nv * 64 * VEC;
-    if (variant) *variant = 500 + nv;
+    const int H = (nv >= 2 && !(one_wave && nv <= 4)) ? 2 : 1;
+    if (variant) *variant = 700 + 10 * (H - 1) + nv;
+    if (H == 1) {
+        switch (nv) {
+        case 1: return launch_block64<S, GRAD, UPD, 1, 1>(L, kp, full, lds, st);
+        case 2: return launch_block64<S, GRAD, UPD, 2, 1>(L, kp, full, lds, st);
+        case 4: return launch_block64<S, GRAD, UPD, 4, 1>(L, kp, full, lds, st);
+        default: return -3;
+        }
+    }
     switch (nv) {
-    case 1: return launch_block64<S, GRAD, UPD, 1>(L, kp, full, lds, st);
-    case 2: return launch_block64<S, GRAD, UPD, 2>(L, kp, full, lds, st);
-    case 4: return launch_block64<S, GRAD, UPD, 4>(L, kp, full, lds, st);
-    case 8: return launch_block64<S, GRAD, UPD, 8>(L, kp, full, lds, st);
+    case 2: return launch_block64<S, GRAD, UPD, 2, 2>(L, kp, full, lds, st);
+    case 4: return launch_block64<S, GRAD, UPD, 4, 2>(L, kp, full, lds, st);
+    case 8: return launch_block64<S, GRAD, UPD, 8, 2>(L, kp, full, lds, st);
     default: return -3;
     }
 }

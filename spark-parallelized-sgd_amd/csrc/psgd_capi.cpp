@@ -219,6 +219,12 @@ struct psgd_ctx {
     // HIP events around the last chain-kernel launch (psgd_ctx_last_chain_ms)
     hipEvent_t ev_begin = nullptr, ev_end = nullptr;
     bool ev_recorded = false;
+    // The scratch buffers above belong to the context, and epochs may run on different caller
+    // streams: each user of them orders its stream after the previous user's work (this event,
+    // recorded on `scratch_stream`) and records the event again when it has enqueued its own.
+    hipEvent_t scratch_ev = nullptr;
+    hipStream_t scratch_stream = nullptr;
+    bool scratch_recorded = false;
 };
 
 namespace {
@@ -377,9 +383,29 @@ int32_t finish_direct(psgd_ctx* ctx, bool any_direct) {
     return PSGD_OK;
 }
 
+// Order `st` after the last work enqueued on the context's scratch buffers from another stream
+// (ctx->mu held).
+int32_t scratch_acquire(psgd_ctx* ctx, hipStream_t st) {
+    if (ctx->scratch_recorded && ctx->scratch_stream != st)
+        HIP_TRY(hipStreamWaitEvent(st, ctx->scratch_ev, 0));
+    return PSGD_OK;
+}
+// `st` now holds the newest work on the scratch buffers (ctx->mu held).
+int32_t scratch_release(psgd_ctx* ctx, hipStream_t st) {
+    if (!ctx->scratch_ev) HIP_TRY(hipEventCreateWithFlags(&ctx->scratch_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(ctx->scratch_ev, st));
+    ctx->scratch_stream = st;
+    ctx->scratch_recorded = true;
+    return PSGD_OK;
+}
+
 // Allocate per-chain buffers and upload descriptors (ctx->mu held).
 int32_t prepare(psgd_ctx* ctx, int32_t d, int state_vectors, hipStream_t st) {
     const size_t P = ctx->parts.size();
+    {
+        const int32_t rc = scratch_acquire(ctx, st);
+        if (rc) return rc;
+    }
     if (ctx->copies_pending) {
         // registration copies still in flight on the copy stream: the epoch waits on the device
         HIP_TRY(hipEventRecord(ctx->copy_ev, ctx->copy_stream));
@@ -507,6 +533,10 @@ int32_t psgd_ctx_destroy(psgd_ctx* ctx) {
         if (ctx->ev_begin) hipEventDestroy(ctx->ev_begin);
         if (ctx->ev_end) hipEventDestroy(ctx->ev_end);
         if (ctx->copy_ev) hipEventDestroy(ctx->copy_ev);
+        if (ctx->scratch_ev) {
+            hipEventSynchronize(ctx->scratch_ev);
+            hipEventDestroy(ctx->scratch_ev);
+        }
         hipStreamDestroy(ctx->copy_stream);
         hipStreamDestroy(ctx->stream);
     }
@@ -800,9 +830,11 @@ int32_t psgd_clear_partitions(psgd_ctx* ctx) {
     if (!ctx) return fail(PSGD_EINVAL, "ctx is null");
     std::lock_guard<std::mutex> lk(ctx->mu);
     DeviceGuard g(ctx->device);
-    // epochs may run on caller streams (psgd_run_epoch_device): drain the device, not just the
-    // context's stream, before the partitions' buffers go
-    hipDeviceSynchronize();
+    // epochs may run on caller streams (psgd_run_epoch_device), each ordered after the previous
+    // one (scratch_acquire): the newest epoch's end and the registration copies are all that
+    // can still read the partitions' buffers
+    if (ctx->scratch_recorded) HIP_TRY(hipEventSynchronize(ctx->scratch_ev));
+    HIP_TRY(hipStreamSynchronize(ctx->copy_stream));
     for (auto& kv : ctx->parts) free_part(kv.second);
     ctx->parts.clear();
     ctx->descs_dirty = true;
@@ -952,6 +984,7 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
     kp.n_chains = P;
     kp.nc = mn ? params->num_classes - 1 : 0;
 
+    bool from_wf32 = false;   // the launch left the chains' weights in L.wf32 (fp32 CSR kernels)
     if (sample_empty) {
         // RDD.sample with fraction 0: every partition is empty -> (w_in, 0, 0, 0) per chain.
         for (int p = 0; p < P; ++p)
@@ -970,13 +1003,14 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         int e = psgd::launch_chains(L, kp, layout, first.dtype == PSGD_F32 ? 1 : 0,
                                     params->compute_dtype == PSGD_F32 ? 1 : 0, params->gradient,
                                     params->updater, conv, min_ld, max_ld,
-                                    lds_spread_bytes(ctx, (size_t)P), st, &ctx->last_variant, max_nnz);
+                                    lds_spread_bytes(ctx, (size_t)P), st, &ctx->last_variant, max_nnz,
+                                    &from_wf32);
         HIP_TRY(hipEventRecord(ctx->ev_end, st));
         ctx->ev_recorded = (e == 0);
         if (L.stamps) {   // PSGD_STAMPS=1: per-chain cycle counters of the CSR fp32 kernels (stderr)
-            // chain_sparse_gram: {chain, loader, gram, apply} x {total, waiting}; chain_sparse_lds:
-            // {chain, loader, tagger} x {total, waiting}; chain_sparse_spec: {chain, helper} x ...
-            const int KS = ctx->last_variant >= 630 ? 16 : ctx->last_variant >= 600 ? 6 : 4;
+            // chain_sparse_lds: {chain, loader, tagger} x {total, waiting}; chain_sparse_spec:
+            // {chain, helper} x {total, waiting}
+            const int KS = ctx->last_variant >= 600 ? 6 : 4;
             std::vector<unsigned long long> h((size_t)P * 16);
             HIP_TRY(hipMemcpyAsync(h.data(), L.stamps, h.size() * 8, hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
@@ -986,12 +1020,9 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
                     v[k].push_back((double)h[(size_t)p * KS + k] / std::max<int64_t>(n_max, 1));
             const char* n4[4] = {"chain.total", "chain.wait", "helper.total", "helper.wait"};
             const char* n6[6] = {"chain.total", "chain.wait", "loader.total", "loader.wait", "tagger.total", "tagger.wait"};
-            const char* n8[16] = {"chain.total", "chain.wait", "loader.total", "loader.wait", "gram.total", "gram.wait",
-                                  "apply.total", "apply.wait", "gram.phaseA", "gram.phaseB", "gram.items", "gram.iters",
-                                  "apply.update", "apply.copy", "apply.dots", "apply.vmwait"};
             for (int k = 0; k < KS; ++k) {
                 std::sort(v[k].begin(), v[k].end());
-                fprintf(stderr, "psgd stamps %-18s cycles/row median %8.1f\n", KS == 16 ? n8[k] : KS == 6 ? n6[k] : n4[k],
+                fprintf(stderr, "psgd stamps %-18s cycles/row median %8.1f\n", KS == 6 ? n6[k] : n4[k],
                         v[k][v[k].size() / 2]);
             }
         }
@@ -999,8 +1030,7 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         if (e) return fail(PSGD_EDEVICE, std::string("chain kernel launch failed: ") +
                                              hipGetErrorString((hipError_t)e));
     }
-    // the fp32 CSR kernels (variants 400-699) leave each chain's weights in L.wf32 (w = alpha v)
-    const bool from_wf32 = !sample_empty && L.wf32 && ctx->last_variant >= 400 && ctx->last_variant < 700;
+    // the fp32 CSR kernels leave each chain's weights in L.wf32 (w = alpha v)
     int e = from_wf32
                 ? psgd::launch_fold_f32(L.wf32, L.wstride, L.walpha, L.rv, L.loss, L.cnt_d, P, dw, d_partial,
                                         L.watchdog, st)
@@ -1009,7 +1039,7 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
     if (d_chain_counts)
         HIP_TRY(hipMemcpyAsync(d_chain_counts, L.cnt, (size_t)P * sizeof(int64_t),
                                hipMemcpyDeviceToDevice, st));
-    return PSGD_OK;
+    return scratch_release(ctx, st);
 }
 
 int32_t psgd_run_epoch(psgd_ctx* ctx, const psgd_params* params, const double* w_in,
@@ -1085,6 +1115,8 @@ int32_t psgd_convergence_terms_device(psgd_ctx* ctx, int32_t d, const double* d_
     std::lock_guard<std::mutex> lk(ctx->mu);
     DeviceGuard g(ctx->device);
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    int32_t rc = scratch_acquire(ctx, st);
+    if (rc) return rc;
     HIP_TRY(ctx->tmp.ensure(((size_t)d + 8) * sizeof(double)));
     double* t = ctx->tmp.as<double>();
     int e = psgd::launch_sq_terms(d_prev, d_cur, d, t, st);
@@ -1106,6 +1138,8 @@ int32_t psgd_initial_regval(psgd_ctx* ctx, const psgd_params* params, int32_t d,
     }
     std::lock_guard<std::mutex> lk(ctx->mu);
     DeviceGuard g(ctx->device);
+    rc = scratch_acquire(ctx, ctx->stream);
+    if (rc) return rc;
     HIP_TRY(ctx->tmp.ensure(((size_t)d + 8) * sizeof(double)));
     double* t = ctx->tmp.as<double>();
     HIP_TRY(hipMemcpyAsync(t + 8, w, (size_t)d * sizeof(double), hipMemcpyHostToDevice, ctx->stream));

@@ -303,7 +303,7 @@ struct RingHeader {
     unsigned ready;     // rows landed in the ring (loader -> compute)
     unsigned consumed;  // rows whose slot may be refilled (compute -> loader)
     unsigned stop;      // compute wave left the chain early (per-sample convergence break)
-    unsigned pad;
+    unsigned consumed1; // a second consumer's `consumed` (chain_block64 with two chain waves)
 };
 // Labels and steps travel in 256-byte meta blocks, one per 16 rows: {y, stepSize/sqrt(j)} x 16.
 constexpr int kMetaRows = 16;
@@ -377,8 +377,9 @@ __device__ __forceinline__ void lds_store_u32_nowait(unsigned* p, unsigned v) {
 
 // GB > 0: rows are also read by two helper waves that take alternate blocks of GB rows and
 // count their finished blocks in gdone[0] (even blocks) / gdone[1] (odd blocks); a slot is free
-// only once both the consumer and its helper are done with it.
-template <typename S, int NV, bool FULL, int PUB, int GB = 0>
+// only once both the consumer and its helper are done with it. CONS = 2: two consumers, the
+// second counting in hdr->consumed1; a slot is free once both have passed it.
+template <typename S, int NV, bool FULL, int PUB, int GB = 0, int CONS = 1>
 __device__ __forceinline__ void ring_loader(const ChainLaunch& L, const ChainDesc& dsc, RingHeader* hdr,
                                             char* meta_ring, char* ring, const RingGeom& geom,
                                             int lane, const unsigned* gdone = nullptr) {
@@ -436,6 +437,10 @@ __device__ __forceinline__ void ring_loader(const ChainLaunch& L, const ChainDes
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             for (;;) {
                 unsigned c = __builtin_amdgcn_readfirstlane(lds_load_u32_asm(&hdr->consumed));
+                if constexpr (CONS == 2) {
+                    const unsigned c1 = __builtin_amdgcn_readfirstlane(lds_load_u32_asm(&hdr->consumed1));
+                    c = c < c1 ? c : c1;
+                }
                 if constexpr (GB > 0) {
                     const unsigned g0 = __builtin_amdgcn_readfirstlane(lds_load_u32_asm(&gdone[0]));
                     const unsigned g1 = __builtin_amdgcn_readfirstlane(lds_load_u32_asm(&gdone[1]));

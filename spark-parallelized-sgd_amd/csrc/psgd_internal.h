@@ -69,9 +69,15 @@ struct ChainLaunch {
 
 // Host-side launchers implemented in psgd_kernels.hip. Return hipError_t as int.
 // storage: 0 = f64, 1 = f32; compute: 0 = f64, 1 = f32.
+// Kernel variants (*kernel_variant, psgd_ctx_last_kernel): 100 + NV chain_dense, 200 + LAYOUT
+// chain_general, 300 + NV chain_block, 400 + storage chain_sparse, 410 + storage chain_sparse_spec,
+// 500 + LAYOUT chain_multinomial, 600+ chain_sparse_lds, 700 + 10 (H - 1) + NV chain_block64.
+// *weights_in_wf32 (nullable): the launch left each chain's weights in L.wf32 (w = walpha v, the
+// fp32 CSR kernels), to be folded by launch_fold_f32; else they are in L.w_out.
 int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int storage, int compute,
                   int gradient, int updater, bool check_conv, int64_t min_ld, int64_t max_ld,
-                  int lds_spread, hipStream_t stream, int* kernel_variant, int64_t max_nnz = 0);
+                  int lds_spread, hipStream_t stream, int* kernel_variant, int64_t max_nnz = 0,
+                  bool* weights_in_wf32 = nullptr);
 // The blocked fp32 kernel (psgd_block.hip): dense rows, Simple/SquaredL2, no per-sample
 // convergence test. launch_block_chains returns -3 when it does not apply.
 bool block_path_applies(int layout, int compute, int updater, bool check_conv, int storage,
@@ -107,12 +113,6 @@ bool sparse_lds_applies(int64_t d, int64_t max_nnz);
 int64_t sparse_lds_head(int64_t d);
 int launch_sparse_lds_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
                              int updater, int64_t max_nnz, hipStream_t stream, int* kernel_variant);
-// The fp32 CSR kernel as a batched scalar recurrence over sparse Gram terms
-// (psgd_sparse_gram.hip): rows of <= 128 non-zeros, features [0, K) in LDS and [K, d) in L.wf32.
-bool sparse_gram_applies(int64_t d, int64_t max_nnz);
-int64_t sparse_gram_head(int64_t d);
-int launch_sparse_gram_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
-                              int updater, int64_t max_nnz, hipStream_t stream, int* kernel_variant);
 // Longest row of a device-resident CSR partition (synchronises `st`).
 int csr_max_nnz(const int64_t* d_row_ptr, int64_t n, int64_t* out, hipStream_t st);
 // RDD.sample(false, fraction, seed) per partition (PSGD.scala:242): from the registered

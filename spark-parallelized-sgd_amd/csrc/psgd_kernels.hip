@@ -879,7 +879,9 @@ static int dispatch_grad(const ChainLaunch& L, const KParams& kp, int layout, in
 
 int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int storage, int compute,
                   int gradient, int updater, bool check_conv, int64_t min_ld, int64_t max_ld,
-                  int lds_spread, hipStream_t stream, int* kernel_variant, int64_t max_nnz) {
+                  int lds_spread, hipStream_t stream, int* kernel_variant, int64_t max_nnz,
+                  bool* weights_in_wf32) {
+    if (weights_in_wf32) *weights_in_wf32 = false;
     if (kp.n_chains <= 0) return 0;
     if (kp.nc > 0)   // LogisticGradient(numClasses > 2)
         return launch_multinomial_chains(L, kp, layout, storage, updater, check_conv, stream, kernel_variant);
@@ -894,8 +896,10 @@ int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int stora
     if (!per_sample && block_path_applies(layout, compute, updater, check_conv, storage, max_ld))
         return launch_block_chains(L, kp, storage, gradient, updater, min_ld, max_ld, lds_spread,
                                    stream, kernel_variant);
-    if (!per_sample && sparse_path_applies(layout, compute, updater, check_conv))
+    if (!per_sample && sparse_path_applies(layout, compute, updater, check_conv)) {
+        if (weights_in_wf32) *weights_in_wf32 = true;
         return launch_sparse_chains(L, kp, storage, gradient, updater, max_nnz, stream, kernel_variant);
+    }
     const size_t lds = (size_t)(lds_spread > 0 ? lds_spread : 0);
     if (storage == 1)
         return dispatch_grad<float>(L, kp, layout, compute, gradient, updater, check_conv, min_ld,

@@ -598,17 +598,12 @@ int launch_sparse_chains(const ChainLaunch& L, const KParams& kp, int storage, i
         return (int)hipErrorInvalidValue;
     int rc = sparse_epoch_init(L, kp, updater, stream);
     if (rc) return rc;
-    // PSGD_SPARSE_KERNEL = gram | lds | spec | plain forces a variant (tests, A/B measurements; read
-    // at every launch); default: the first that applies in that order
+    // PSGD_SPARSE_KERNEL = lds | spec | plain forces a variant (tests, A/B measurements; read at
+    // every launch); default: the first that applies in that order
     const char* force = getenv("PSGD_SPARSE_KERNEL");
     const bool any = !force || !*force;
     const bool no_lds = !any && strcmp(force, "lds") != 0;
     const bool no_spec = !any && strcmp(force, "spec") != 0;
-    const bool gram = !any && strcmp(force, "gram") == 0;
-    if (gram) {
-        rc = launch_sparse_gram_chains(L, kp, storage, gradient, updater, max_nnz, stream, kernel_variant);
-        if (rc != -3) return rc;
-    }
     // first choice: the chain's weights in LDS (psgd_sparse_lds.hip), for rows of <= 128
     // non-zeros and d up to ~65k features
     if (!no_lds) {

@@ -209,6 +209,9 @@ class HipEngine(ShardedEngine):
             return super().epoch(params, w_dev, with_counts)
 
     def local_partial(self, params, w_dev, with_counts):
+        # The lock serialises re-registration and the enqueue; the device order of epochs that
+        # share the context's scratch buffers from different streams is the library's
+        # (psgd_run_epoch_device waits for the previous epoch's end event on another stream).
         with self.ctx.engine_lock:
             # another engine on this device may have registered its own partitions since
             if self.ctx.registered_token != self._key:

@@ -176,11 +176,13 @@ def test_dense_fp32_throughput_updaters(pkg, oracle, upd, d, dtype):
 
 
 def test_kernel_selection(pkg, oracle):
-    """fp64 compute: tol = 0 with Simple/SquaredL2 runs the blocked fp64 kernel (50x), tol > 0
-    the per-sample chain_dense (10x), d past the register-resident range chain_general (200)."""
+    """fp64 compute: tol = 0 with Simple/SquaredL2 runs the blocked fp64 kernel (70x one chain
+    wave, 71x two), tol > 0 the per-sample chain_dense (10x), d past the register-resident range
+    chain_general (200)."""
     rng = np.random.default_rng(1)
-    for d, dtype, tol, expect in ((100, np.float64, 0.0, 501), (512, np.float32, 0.0, 502),
-                                  (1024, np.float32, 0.0, 504), (2048, np.float32, 0.0, 508),
+    for d, dtype, tol, expect in ((100, np.float64, 0.0, 701), (512, np.float32, 0.0, 712),
+                                  (1024, np.float32, 0.0, 714), (2048, np.float32, 0.0, 718),
+                                  (1024, np.float64, 0.0, 718),
                                   (100, np.float64, 0.001, 101), (512, np.float32, 0.001, 102),
                                   (3000, np.float64, 0.0, 200)):
         X, y = synth(rng, 64, d, "logistic", dtype)
@@ -438,25 +440,29 @@ def test_libsvm_file_to_chains(pkg, oracle, tmp_path):
 @pytest.mark.parametrize("d", [100, 300, 700, 1024])
 @pytest.mark.parametrize("grad", ["least_squares", "logistic", "hinge"])
 @pytest.mark.parametrize("upd", ["simple", "squared_l2"])
-def test_fp64_block_f32_rows_in_registers(pkg, oracle, d, grad, upd):
-    """chain_block64 on f32 rows (NV = 1, 2, 4; the c2 / c3 fp64 instances): the block's rows are
-    held in registers as stored and converted where used. d = 100 / 300 / 700 exercise the
-    zero-masked row end, 903-row partitions a ragged last block; 1e-9 and exact counts against
-    the oracle."""
+@pytest.mark.parametrize("storage", [np.float32, np.float64])
+def test_fp64_block_rows_in_registers(pkg, oracle, d, grad, upd, storage):
+    """chain_block64 (NV = 1, 2, 4 f32 / 1, 2, 4, 8 f64; the c2 / c3 fp64 instances, f32 and the
+    reference's Double rows): one chain wave at NV = 1, else two chain waves that split the
+    features and exchange their partial dots per block, every row of a block held in registers.
+    d = 100 / 300 / 700 exercise the zero-masked row end, 903-row partitions a ragged last block;
+    1e-9 and exact counts against the oracle."""
     rng = np.random.default_rng(d + len(grad) * 3 + len(upd))
     n, P = 2709, 3
     X, y = synth(rng, n, d, grad, np.float32)
-    data = pkg.PartitionedData.parallelize(y, X, P, dtype=np.float32)
+    data = pkg.PartitionedData.parallelize(y, X.astype(storage), P, dtype=storage)
     offs = [i * n // P for i in range(P)] + [n]
     step = 2.0 / d if grad == "logistic" else 0.5 / d   # non-chaotic trajectories (1e-9 bar)
     G = {"logistic": pkg.LogisticGradient, "least_squares": pkg.LeastSquaresGradient, "hinge": pkg.HingeGradient}
     U = {"simple": pkg.SimpleSGDUpdater, "squared_l2": pkg.SquaredL2SGDUpdater}
     w, h, counts = pkg.runParallelizedSGD(data, G[grad](), U[upd](), step, 3, 0.05, 1.0, np.zeros(d), 0.0,
                                           return_chain_counts=True)
+    vec = 4 if storage == np.float32 else 2
     nv = 1
-    while nv * 256 < d:
+    while nv * 64 * vec < d:
         nv *= 2
-    assert pkg.optimization.get_context(0).last_kernel() == 500 + nv
+    waves = 2 if nv >= 2 else 1
+    assert pkg.optimization.get_context(0).last_kernel() == 700 + 10 * (waves - 1) + nv
     wr, hr, cr = oracle.run(oracle.Matrix(y, X.astype(np.float64)), offs, grad, upd, step, 3, 0.05,
                             np.zeros(d), tol=0.0, n_threads=8)
     assert [list(c) for c in counts] == [list(c) for c in cr[: len(counts)]]

@@ -1,7 +1,6 @@
 """The fp32 CSR chain kernels (psgd_sparse_lds.hip, psgd_sparse.hip) against the fp64 CPU oracle.
 
-Every case runs on each kernel variant (PSGD_SPARSE_KERNEL forces one): chain_sparse_gram (the
-batched Gram recurrence) with all weights in LDS and with an LDS head of d/3, chain_sparse_lds with
+Every case runs on each kernel variant (PSGD_SPARSE_KERNEL forces one): chain_sparse_lds with
 all weights in LDS, with an LDS head of d/3 features and the rest in HBM (PSGD_SPARSE_LDS_HEAD:
 exercises the tail gathers and their corrections at small d) at speculation depths 4 and 8,
 chain_sparse_spec, and chain_sparse.
@@ -36,8 +35,6 @@ def need_gpu():
 
 
 KERNELS = {  # name: (environment, variant base without the storage digit)
-    "gram": ({"PSGD_SPARSE_KERNEL": "gram"}, 630),
-    "gram_tail": ({"PSGD_SPARSE_KERNEL": "gram", "PSGD_SPARSE_LDS_HEAD": "third"}, 630),
     "lds": ({"PSGD_SPARSE_KERNEL": "lds"}, 600),
     "lds_tail": ({"PSGD_SPARSE_KERNEL": "lds", "PSGD_SPARSE_LDS_HEAD": "third"}, 600),
     "lds_tail_sk8": ({"PSGD_SPARSE_KERNEL": "lds", "PSGD_SPARSE_LDS_HEAD": "third", "PSGD_SPARSE_SK": "8"}, 610),

@@ -1,4 +1,5 @@
-"""CPU model of chain_sparse_gram's algorithm (psgd_sparse_gram.hip), checked against the
+"""CPU model of chain_sparse_gram's algorithm (tools/experimental/psgd_sparse_gram.hip: a measured
+negative result kept out of libpsgd.so), checked against the
 sequential chain of ParallelizedSGD.scala:243-270 in f64.
 
 The kernel splits a CSR chain into batches of 8 rows and takes each row's dot against a weight

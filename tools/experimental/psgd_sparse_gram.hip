@@ -1,3 +1,6 @@
+// NOT BUILT: a measured negative result (DESIGN.md §3, 342 vs 573 M samples/s for
+// chain_sparse_lds at c4), moved out of libpsgd.so in round 3. It compiles only against the
+// round-2 tree (git history: spark-parallelized-sgd_amd/csrc/psgd_sparse_gram.hip).
 // psgd_sparse_gram.hip -- the fp32 CSR chain as a batched scalar recurrence over sparse Gram
 // terms (gfx950).
 //
