@@ -70,7 +70,8 @@ def pmc_traffic(workload, grad, variant, storage, rows, compute="f32", updater="
         prefix = f"psgd::chain_block64<{sname}, {g}, {u}, {variant % 10}, "
         waves = 1 + (variant - 700) // 10
     elif variant >= 600:
-        prefix = f"psgd::chain_sparse_lds<{sname}, {g}, {u},"
+        tname = "double" if (variant % 100) >= 20 else "float"
+        prefix = f"psgd::chain_sparse_lds<{sname}, {tname}, {g}, {u},"
     elif variant >= 500:
         prefix = f"psgd::chain_block64<{sname}, {g}, {u}, {variant - 500},"
     elif variant >= 410:
@@ -101,8 +102,9 @@ def kernel_name(variant):
     if 300 <= variant < 400:
         return f"chain_block (NV={variant - 300}: blocked fp32 chain, 8-row Gram blocks)"
     if 600 <= variant < 700:
-        return (f"chain_sparse_lds (fp32 CSR chain, weights LDS-resident [tail past ~160 KiB: L2-resident, "
-                f"gathered {8 if variant >= 610 else 4} samples ahead with an LDS feature-tag correction])")
+        prec = "fp64" if (variant % 100) >= 20 else "fp32"
+        return (f"chain_sparse_lds ({prec} CSR chain, weights LDS-resident [tail past ~160 KiB: L2-resident, "
+                f"gathered {8 if (variant % 20) >= 10 else 4} samples ahead with an LDS feature-tag correction])")
     if 410 <= variant < 420:
         return ("chain_sparse_spec (fp32 CSR chain, weights L2/MALL-resident, gathers 8 samples "
                 "ahead with an LDS feature-tag correction)")

@@ -141,6 +141,48 @@ __device__ __forceinline__ double row_loss64(double z, double y) {
 
 }  // namespace
 
+// The SIMD a wave runs on (HW_REG_HW_ID bits 5:4).
+__device__ __forceinline__ unsigned wave_simd() {
+    unsigned id;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(id));
+    return (id >> 4) & 3;
+}
+
+// Role of wave w given every wave's SIMD (3 + H waves; the same answer in every wave). Roles:
+// 0 .. H-1 chain waves, then (H = 1) 1 loader, 2, 3 Gram waves / (H = 2) 2, 3 Gram waves,
+// 4 loader. The dispatcher does not promise which SIMD a wave of a workgroup lands on, and the
+// chain waves are the critical path: the first chain wave is wave 0, the second the first wave on
+// another SIMD (one it has to itself if there is one); the loader (it mostly sleeps on the
+// ring) takes a SIMD a chain wave is on if any remaining wave is, so the Gram waves do not.
+template <int H>
+__device__ __forceinline__ int role_of_wave(const unsigned* simd, int w) {
+    constexpr int NW = 3 + H;
+    int count[4] = {0, 0, 0, 0};
+    for (int i = 0; i < NW; ++i) ++count[simd[i] & 3];
+    int role[NW];
+    for (int i = 0; i < NW; ++i) role[i] = -1;
+    role[0] = 0;
+    int c1 = -1;
+    if constexpr (H == 2) {
+        for (int i = 1; i < NW && c1 < 0; ++i)
+            if (simd[i] != simd[0] && count[simd[i] & 3] == 1) c1 = i;
+        for (int i = 1; i < NW && c1 < 0; ++i)
+            if (simd[i] != simd[0]) c1 = i;
+        if (c1 < 0) c1 = 1;
+        role[c1] = 1;
+    }
+    int ld = -1;
+    for (int i = 1; i < NW && ld < 0; ++i)
+        if (role[i] < 0 && (simd[i] == simd[0] || (c1 >= 0 && simd[i] == simd[c1]))) ld = i;
+    for (int i = NW - 1; i >= 1 && ld < 0; --i)
+        if (role[i] < 0) ld = i;
+    role[ld] = H == 1 ? 1 : 4;
+    int g = 2;
+    for (int i = 1; i < NW; ++i)
+        if (role[i] < 0) role[i] = g++;
+    return role[w];
+}
+
 // The chain waves of one chain (H = 2) exchange their partial dots through LDS once per block:
 // per block parity and chain wave, one partial per row; at the chain's end, the partial ||w||^2.
 struct XchgHeader64 {
@@ -171,9 +213,8 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
     static_assert(NV % H == 0, "the chain waves split the row slices evenly");
     static_assert(EH <= (F32 ? 16 : 8), "a chain wave keeps its share of a block's rows in registers");
     constexpr bool CONV1 = F32 && H == 2 && EH <= 8 && PSGD_B64_CONV1;
-    // wave roles: chain waves 0 .. H-1, Gram waves 2 and 3, the loader (H = 2: wave 4, which
-    // shares the first chain wave's SIMD; it mostly sleeps on the ring)
-    constexpr int kLoaderWave = H == 1 ? 1 : 4;
+    // wave roles (role_of_waves): chain waves 0 .. H-1, Gram waves 2 and 3, the loader
+    constexpr int kRoleLoader = H == 1 ? 1 : 4;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // LDS: [RingHeader 16 B][GramHeader64 16 B][XchgHeader64 16 B][exchange 34 doubles]
     //      [meta ring MB x 256 B][Gram ring GS x 512 B][row ring R x ROW_BYTES]
@@ -187,7 +228,6 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
     char* ring = reinterpret_cast<char*>(gring + GS * kB * kB);
 
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
     const int chain = blockIdx.x;
     const ChainDesc dsc = L.descs[chain];
     const int d = kp.d;
@@ -212,9 +252,14 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
     }
     // entries on and above the diagonal stay zero (the Gram waves write only i < k)
     for (int i = threadIdx.x; i < GS * kB * kB; i += blockDim.x) gring[i] = 0.0;
+    // every wave's SIMD, for the role assignment (the exchange area is free until the chain starts)
+    unsigned* simd_of = reinterpret_cast<unsigned*>(xchg);
+    if (lane == 0) simd_of[threadIdx.x >> 6] = wave_simd();
     __syncthreads();
+    const int wave = __builtin_amdgcn_readfirstlane(role_of_wave<H>(simd_of, threadIdx.x >> 6));
+    __syncthreads();   // the SIMD table is read by every wave before the exchange area is used
 
-    if (wave == kLoaderWave) {
+    if (wave == kRoleLoader) {
         ring_loader<S, NV, FULL, kB, kB, H>(L, dsc, hdr, meta_ring, ring, geom, lane, ghdr->gread);
         return;
     }

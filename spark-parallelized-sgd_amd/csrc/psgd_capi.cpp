@@ -225,6 +225,10 @@ struct psgd_ctx {
     hipEvent_t scratch_ev = nullptr;
     hipStream_t scratch_stream = nullptr;
     bool scratch_recorded = false;
+    // alpha_in_range's cached answer
+    int64_t alpha_n = -1;
+    double alpha_step = NAN, alpha_reg = NAN;
+    bool alpha_ok = false;
 };
 
 namespace {
@@ -448,6 +452,25 @@ int32_t prepare(psgd_ctx* ctx, int32_t d, int state_vectors, hipStream_t st) {
         ctx->descs_dirty = false;
     }
     return PSGD_OK;
+}
+
+// SquaredL2's alpha-scaled CSR form without renormalisation (the fp64 chain_sparse_lds) is
+// valid when every prefix product of (1 - s_j lambda), s_j = stepSize / sqrt(j) as the steps
+// kernel computes it, stays finite, non-zero and in [2^-400, 2^400] (chain_general's
+// renormalisation bounds) for j up to the longest chain. Cached per (step, lambda, n).
+bool alpha_in_range(psgd_ctx* ctx, double step, double reg, int64_t n) {
+    if (ctx->alpha_n == n && ctx->alpha_step == step && ctx->alpha_reg == reg) return ctx->alpha_ok;
+    double a = 1.0;
+    bool ok = true;
+    for (int64_t j = 1; j <= n && ok; ++j) {
+        a *= 1.0 - (step / std::sqrt((double)j)) * reg;
+        ok = std::fabs(a) >= 0x1p-400 && std::fabs(a) <= 0x1p400;
+    }
+    ctx->alpha_n = n;
+    ctx->alpha_step = step;
+    ctx->alpha_reg = reg;
+    ctx->alpha_ok = ok;
+    return ok;
 }
 
 int32_t ensure_steps(psgd_ctx* ctx, double step, int64_t n, hipStream_t st) {
@@ -959,6 +982,13 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         L.walpha = ctx->walpha.as<double>();
         L.wnsq0 = ctx->wnsq0.as<double>();
     }
+    if (layout == psgd::kCsr && params->compute_dtype == PSGD_F64 && !mn &&
+        psgd::sparse_lds64_applies(d, max_nnz, params->updater, conv, true)) {
+        // the fp64 CSR kernel's per-chain f64 vectors (d + 1152 doubles, in L.wf32's memory)
+        L.wstride = 2 * (((int64_t)d + 128 + 1024 + 63) / 64 * 64);
+        HIP_TRY(ctx->wf32.ensure((size_t)P * (size_t)L.wstride * sizeof(float)));
+        L.wf32 = ctx->wf32.as<float>();
+    }
     if (params->gradient == PSGD_GRADIENT_LOGISTIC && params->compute_dtype == PSGD_F32 &&
         layout == psgd::kDense) {
         // per-row margins of the fp32 Logistic block kernel (its loss is summed after the chain)
@@ -983,6 +1013,8 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
     kp.d = d;
     kp.n_chains = P;
     kp.nc = mn ? params->num_classes - 1 : 0;
+    kp.alpha_ok = params->updater != PSGD_UPDATER_SQUARED_L2 ||
+                  alpha_in_range(ctx, params->step_size, params->reg_param, n_max);
 
     bool from_wf32 = false;   // the launch left the chains' weights in L.wf32 (fp32 CSR kernels)
     if (sample_empty) {

@@ -26,6 +26,10 @@ struct KParams {
     int32_t d;                // features per row
     int32_t n_chains;
     int32_t nc = 0;           // multinomial LogisticGradient: K - 1 weight blocks of d; 0: binary
+    // SquaredL2's alpha-scaled CSR form without renormalisation is valid for this epoch: every
+    // prefix product of (1 - s_j lambda), j <= the longest chain, is finite, non-zero and within
+    // [2^-400, 2^400] (set by the host; chain_sparse_lds in fp64 runs only then)
+    int32_t alpha_ok = 0;
 };
 
 // LogisticGradient(numClasses = K): at most this many weight blocks (K - 1), the chain keeps
@@ -71,7 +75,8 @@ struct ChainLaunch {
 // storage: 0 = f64, 1 = f32; compute: 0 = f64, 1 = f32.
 // Kernel variants (*kernel_variant, psgd_ctx_last_kernel): 100 + NV chain_dense, 200 + LAYOUT
 // chain_general, 300 + NV chain_block, 400 + storage chain_sparse, 410 + storage chain_sparse_spec,
-// 500 + LAYOUT chain_multinomial, 600+ chain_sparse_lds, 700 + 10 (H - 1) + NV chain_block64.
+// 500 + LAYOUT chain_multinomial, 600 + 10 (SK 8) + 20 (fp64) + storage chain_sparse_lds,
+// 700 + 10 (H - 1) + NV chain_block64.
 // *weights_in_wf32 (nullable): the launch left each chain's weights in L.wf32 (w = walpha v, the
 // fp32 CSR kernels), to be folded by launch_fold_f32; else they are in L.w_out.
 int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int storage, int compute,
@@ -113,6 +118,12 @@ bool sparse_lds_applies(int64_t d, int64_t max_nnz);
 int64_t sparse_lds_head(int64_t d);
 int launch_sparse_lds_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
                              int updater, int64_t max_nnz, hipStream_t stream, int* kernel_variant);
+// The same kernel in fp64 compute (the parity mode's CSR throughput kernel): Simple, and
+// SquaredL2 when kp.alpha_ok; the chain's f64 vector lives in its slice of L.wf32, which must be
+// >= 2 (d + 1152) floats; weights end in L.w_out. -3 when it does not apply.
+bool sparse_lds64_applies(int64_t d, int64_t max_nnz, int updater, bool check_conv, bool alpha_ok);
+int launch_sparse_lds64_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
+                               int updater, int64_t max_nnz, hipStream_t stream, int* kernel_variant);
 // Longest row of a device-resident CSR partition (synchronises `st`).
 int csr_max_nnz(const int64_t* d_row_ptr, int64_t n, int64_t* out, hipStream_t st);
 // RDD.sample(false, fraction, seed) per partition (PSGD.scala:242): from the registered

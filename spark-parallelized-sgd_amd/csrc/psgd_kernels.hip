@@ -228,9 +228,15 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, Ri
                 const T2 g = mult * x[e];
                 const T2 acc2 = first ? g * g : ua[e] + g * g;
                 ua[e] = acc2;
-                // fp32 mode: g * rsqrt(accum + 1) (one v_rsq_f32, ~1 ulp) for g / sqrt(accum + 1)
-                nw.x = old.x + a * (g.x * __builtin_amdgcn_rsqf(acc2.x + T(1)));
-                nw.y = old.y + a * (g.y * __builtin_amdgcn_rsqf(acc2.y + T(1)));
+                if constexpr (sizeof(T) == 4) {
+                    // fp32 mode: g * rsqrt(accum + 1) (one v_rsq_f32, ~1 ulp) for g / sqrt(accum + 1)
+                    nw.x = old.x + a * (g.x * __builtin_amdgcn_rsqf(acc2.x + T(1)));
+                    nw.y = old.y + a * (g.y * __builtin_amdgcn_rsqf(acc2.y + T(1)));
+                } else {
+                    // pow(accum + 1.0, 0.5) as the correctly rounded sqrt (UPD.scala:209)
+                    nw.x = old.x + a * (g.x / m_sqrt(acc2.x + T(1)));
+                    nw.y = old.y + a * (g.y / m_sqrt(acc2.y + T(1)));
+                }
             } else if constexpr (UPD == U_ADAM) {
                 // the reference's variant, literally: v = beta v + (1-beta) g,
                 // r = gamma r + (1-gamma) g^2, fix1 = sqrt(1 - r^iter) + eps, w += -lr * v / fix1
@@ -809,11 +815,15 @@ static int dispatch_nv(const ChainLaunch& L, const KParams& kp, int64_t min_ld, 
     // FULL: every lane's every vector is inside every row (no exec masking on the loads).
     const bool full = min_ld >= (int64_t)nv * 64 * VEC;
     if (variant) *variant = 100 + nv;
+    // fp64 AdaGrad / Adam hold at most 16 doubles per lane (dispatch_layout): no NV past that
+    constexpr int NVMAX = (sizeof(T) == 8 && UPD >= U_ADAGRAD) ? 16 / VEC : 8;
     switch (nv) {
     case 1: return launch_reg<S, T, GRAD, UPD, CONV, 1>(L, kp, full, lds, st);
     case 2: return launch_reg<S, T, GRAD, UPD, CONV, 2>(L, kp, full, lds, st);
     case 4: return launch_reg<S, T, GRAD, UPD, CONV, 4>(L, kp, full, lds, st);
-    case 8: return launch_reg<S, T, GRAD, UPD, CONV, 8>(L, kp, full, lds, st);
+    case 8:
+        if constexpr (NVMAX >= 8) return launch_reg<S, T, GRAD, UPD, CONV, 8>(L, kp, full, lds, st);
+        return -1;
     default: return -1;
     }
 }
@@ -836,10 +846,13 @@ static int dispatch_layout(const ChainLaunch& L, const KParams& kp, int layout, 
             return dispatch_nv<S, double, GRAD, UPD, CONV>(L, kp, min_ld, max_ld, lds, st, variant);
         }
     } else {
-        // AdaGrad / Adam in the fp32 throughput mode: weights and status in registers (the fp64
-        // parity mode keeps chain_general, status in HBM)
+        // AdaGrad / Adam: weights and status in registers. fp32: up to 8 row vectors per lane;
+        // fp64 (the parity mode): up to 16 doubles per lane (weights, status and two row buffers
+        // are 5 x 16 doubles = 160 VGPRs), d <= 1,024; past that chain_general, status in HBM
         if (layout == kDense && compute == 1 && max_ld <= 8 * 64 * VEC)
             return dispatch_nv<S, float, GRAD, UPD, CONV>(L, kp, min_ld, max_ld, lds, st, variant);
+        if (layout == kDense && compute == 0 && max_ld <= 16 * 64)
+            return dispatch_nv<S, double, GRAD, UPD, CONV>(L, kp, min_ld, max_ld, lds, st, variant);
     }
     if (layout == kDense) return launch_gen<S, kDense, GRAD, UPD, CONV>(L, kp, st, variant);
     return launch_gen<S, kCsr, GRAD, UPD, CONV>(L, kp, st, variant);
@@ -900,6 +913,9 @@ int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int stora
         if (weights_in_wf32) *weights_in_wf32 = true;
         return launch_sparse_chains(L, kp, storage, gradient, updater, max_nnz, stream, kernel_variant);
     }
+    if (!per_sample && layout == kCsr && compute == 0 &&
+        sparse_lds64_applies(kp.d, max_nnz, updater, check_conv, kp.alpha_ok != 0) && L.wf32)
+        return launch_sparse_lds64_chains(L, kp, storage, gradient, updater, max_nnz, stream, kernel_variant);
     const size_t lds = (size_t)(lds_spread > 0 ? lds_spread : 0);
     if (storage == 1)
         return dispatch_grad<float>(L, kp, layout, compute, gradient, updater, check_conv, min_ld,

@@ -1,9 +1,19 @@
-// psgd_sparse_lds.hip -- the fp32 CSR chain with the chain's weights resident in LDS (gfx950).
+// psgd_sparse_lds.hip -- the CSR chain with the chain's weights resident in LDS (gfx950): fp32
+// compute (the throughput mode) and fp64 compute (the parity mode's CSR throughput kernel).
 //
 // Reference: ParallelizedSGD.scala:243-270 (the chain: weights read by Gradient.compute at :254,
 // written by SGDUpdater.compute at :255-256), [ext] MLlib 1.6.1 Gradient.scala on SparseVector rows
 // (the gradient is mult * x, non-zero only at the row's indices), SGDUpdater.scala:86-98 (Simple)
 // and :163-181 (SquaredL2, alpha-scaled lazy form as in psgd_sparse.hip).
+//
+// T = float: weights as fp32, the tail in L.wf32, folded from there (launch_fold_f32).
+// T = double: every weight, the LDS head and the HBM tail, is a double (the tail in the chain's
+// slice of L.wf32 viewed as doubles); the coefficient, the loss and SquaredL2's alpha are the
+// reference's Double arithmetic (only the dot's wave tree and the fused c*x + w are reassociated,
+// the fp64 mode's 1e-9 bar); at the chain's end w = alpha v goes to L.w_out (the f64 fold) and
+// regVal is taken from it. The alpha-scaled form runs without renormalisation, so the host
+// launches it only when every prefix product of (1 - s_j lambda) stays in [2^-400, 2^400]
+// (kp.alpha_ok); otherwise chain_general, which renormalises, runs.
 //
 // One workgroup = one chain = one CU (the 160 KiB LDS holds one chain's weights). Features
 // [0, K) live in LDS as fp32 ("head"); when d does not fit, features [K, d) ("tail") stay in the
@@ -60,6 +70,17 @@ __device__ __forceinline__ float buffer_gather_sc1(i32x4 rsrc, uint32_t off) {
 __device__ __forceinline__ void buffer_store_f32(i32x4 rsrc, uint32_t off, float v) {
     asm volatile("buffer_store_dword %0, %1, %2, 0 offen" : : "v"(v), "v"(off), "s"(rsrc) : "memory");
 }
+__device__ __forceinline__ double buffer_gather_sc1(i32x4 rsrc, uint32_t off, double) {
+    double v;
+    asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen sc1" : "=v"(v) : "v"(off), "s"(rsrc) : "memory");
+    return v;
+}
+__device__ __forceinline__ float buffer_gather_sc1(i32x4 rsrc, uint32_t off, float) {
+    return buffer_gather_sc1(rsrc, off);
+}
+__device__ __forceinline__ void buffer_store_f32(i32x4 rsrc, uint32_t off, double v) {
+    asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen" : : "v"(v), "v"(off), "s"(rsrc) : "memory");
+}
 constexpr int kMetaRing = 128;             // rows of label / step / nnz
 constexpr int kSweepRows = 128;            // the tag table is swept once per this many rows
 constexpr int64_t kLdsCap = 160 * 1024;    // LDS per CU (gfx950)
@@ -82,56 +103,73 @@ struct LdsHeader {
     unsigned dtag;     // target of inactive lanes' tag reads and writes
     unsigned pad[2];
 };
+template <typename T>
 struct LdsMeta {
-    float y[kMetaRing];
-    float s[kMetaRing];       // stepSize / sqrt(j), rounded (fp32 compute)
+    T y[kMetaRing];
+    T s[kMetaRing];           // stepSize / sqrt(j) (rounded to fp32 in fp32 compute)
     double s64[kMetaRing];    // the same in f64 (SquaredL2's alpha)
     int32_t nnz[kMetaRing];
 };
+template <typename T>
 struct LdsSlot {
     int32_t col[LCAP];   // feature index
-    float val[LCAP];     // x_j; the chain replaces a tail entry's x_j by its new weight
+    T val[LCAP];         // x_j; the chain replaces a tail entry's x_j by its new weight
     uint32_t rw[LCAP];   // LDS dword addresses: read (bits 0-15), write (bits 16-31)
 };
-constexpr unsigned kLdsDummy = 4;              // dword index of LdsHeader::dummy
+// dword index of the target of inactive entries' weight reads and writes (LdsHeader::dummy; an
+// 8-byte aligned pair, pad[0..1], for doubles)
+template <typename T>
+constexpr unsigned lds_dummy() { return sizeof(T) == 8 ? 6 : 4; }
 constexpr int64_t kMetaOff = sizeof(LdsHeader);
-constexpr int64_t kSlotOff = kMetaOff + sizeof(LdsMeta);
-static_assert(kSlotOff % 16 == 0 && sizeof(LdsSlot) % 16 == 0, "alignment");
+template <typename T>
+constexpr int64_t slot_off() { return kMetaOff + (int64_t)sizeof(LdsMeta<T>); }
+static_assert(slot_off<float>() % 16 == 0 && sizeof(LdsSlot<float>) % 16 == 0, "alignment");
+static_assert(slot_off<double>() % 16 == 0 && sizeof(LdsSlot<double>) % 16 == 0, "alignment");
 
-template <int SK>
-constexpr int64_t lds_fixed_bytes() { return kSlotOff + LdsRing<SK>::SR * (int64_t)sizeof(LdsSlot); }
+template <int SK, typename T>
+constexpr int64_t lds_fixed_bytes() { return slot_off<T>() + LdsRing<SK>::SR * (int64_t)sizeof(LdsSlot<T>); }
 // tail tag table entries (u16), rounded for the sweep's 4-tag accesses
 __host__ __device__ inline int64_t tag_entries(int64_t d, int64_t K) { return ((d - K) + 3) & ~int64_t(3); }
-template <int SK>
-int64_t lds_bytes(int64_t d, int64_t K) { return lds_fixed_bytes<SK>() + 4 * K + 2 * tag_entries(d, K); }
+template <int SK, typename T>
+int64_t lds_bytes(int64_t d, int64_t K) {
+    return lds_fixed_bytes<SK, T>() + (int64_t)sizeof(T) * K + 2 * tag_entries(d, K);
+}
 // Features [0, K) in LDS: all of them when they fit, else as many as leave room for the tail's
 // tag table (K a multiple of 4: the table stays 8-byte aligned); -1 when not even the table fits.
-template <int SK>
+template <int SK, typename T>
 int64_t lds_head(int64_t d) {
-    const int64_t budget = kLdsCap - lds_fixed_bytes<SK>();
-    if (4 * d <= budget) return d;
-    int64_t K = (budget - 2 * (d + 4)) / 2;
+    const int64_t budget = kLdsCap - lds_fixed_bytes<SK, T>();
+    if ((int64_t)sizeof(T) * d <= budget) return d;
+    int64_t K = (budget - 2 * (d + 4)) / ((int64_t)sizeof(T) - 2);
     K &= ~int64_t(3);
     return K >= 0 ? K : -1;
 }
 
 // TAIL = false: every feature is in LDS (K = d), the chain issues no VMEM at all.
-template <typename S, int GRAD, int UPD, int SK, bool TAIL>
+// T: the weights' and the arithmetic's type (float: the fp32 throughput mode; double: fp64).
+template <typename S, typename T, int GRAD, int UPD, int SK, bool TAIL>
 __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams kp, int K) {
     constexpr bool L2 = UPD == U_SQUARED_L2;
+    constexpr bool F64 = sizeof(T) == 8;
     constexpr int SR = LdsRing<SK>::SR;
+    constexpr unsigned WD = sizeof(T) / 4;                       // dwords per weight
+    constexpr unsigned kLdsDummy = lds_dummy<T>();
+    constexpr int64_t kSlotOff = slot_off<T>();
     static_assert((SR & (SR - 1)) == 0, "slot index by mask");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     LdsHeader* hdr = reinterpret_cast<LdsHeader*>(smem);
-    LdsMeta* meta = reinterpret_cast<LdsMeta*>(smem + kMetaOff);
-    LdsSlot* slots = reinterpret_cast<LdsSlot*>(smem + kSlotOff);
+    LdsMeta<T>* meta = reinterpret_cast<LdsMeta<T>*>(smem + kMetaOff);
+    LdsSlot<T>* slots = reinterpret_cast<LdsSlot<T>*>(smem + kSlotOff);
     float* lds = reinterpret_cast<float*>(smem);                 // dword-addressed view
-    constexpr unsigned kWoff = (unsigned)(lds_fixed_bytes<SK>() / 4);
-    float* W = lds + kWoff;                                      // head weights [K]
+    // a weight (or a slot's value) at dword index i
+    auto ld_w = [&](unsigned i) __attribute__((always_inline)) -> T { return *reinterpret_cast<const T*>(lds + i); };
+    auto st_w = [&](unsigned i, T v) __attribute__((always_inline)) { *reinterpret_cast<T*>(lds + i) = v; };
+    constexpr unsigned kWoff = (unsigned)(lds_fixed_bytes<SK, T>() / 4);
+    T* W = reinterpret_cast<T*>(lds + kWoff);                    // head weights [K]
     uint16_t* tagpos = reinterpret_cast<uint16_t*>(W + K);       // tail features K .. d-1
     // dword index of val[0] of the slot holding row u
     auto val_off = [](int64_t u) __attribute__((always_inline)) -> unsigned {
-        return (unsigned)((kSlotOff + (int64_t)(u & (SR - 1)) * (int64_t)sizeof(LdsSlot)) / 4) + LCAP;
+        return (unsigned)((kSlotOff + (int64_t)(u & (SR - 1)) * (int64_t)sizeof(LdsSlot<T>)) / 4) + LCAP;
     };
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -139,20 +177,26 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
     const ChainDesc dsc = L.descs[chain];
     const int d = kp.d;
     const int64_t n = dsc.n_rows;
-    const int64_t T = tag_entries(d, K);
+    const int64_t NT = tag_entries(d, K);
     // The chain runs n_pad samples (a multiple of its unroll SK + 1) and reads up to row
     // n_pad + SK ahead: the loader and the tagger stage n_fill rows, rows past n null (no
     // entries, label and step 0), so no read in the chain needs a condition.
     constexpr int GS = SK + 1;
     const int64_t n_pad = (n + GS - 1) / GS * GS;
     const int64_t n_fill = (n_pad + SK + 1 + 7) / 8 * 8;
-    // [d] (tail used) + [128] the loader's dummy sources + [1024] the chain's dummy targets
-    float* V = L.wf32 + (int64_t)chain * L.wstride;
+    // [d] (tail used) + [128] the loader's dummy sources + [1024] the chain's dummy targets (in
+    // T: for doubles the chain's slice of L.wf32 is twice as long, launch_sparse_lds64_chains)
+    T* V = reinterpret_cast<T*>(L.wf32 + (int64_t)chain * L.wstride);
 
-    for (int64_t i = threadIdx.x; i < T; i += blockDim.x) tagpos[i] = 0xFFFF;
-    for (int i = threadIdx.x; i < K; i += blockDim.x) W[i] = float(as_global(L.w_in)[i]);
+    for (int64_t i = threadIdx.x; i < NT; i += blockDim.x) tagpos[i] = 0xFFFF;
+    for (int i = threadIdx.x; i < K; i += blockDim.x) W[i] = T(as_global(L.w_in)[i]);
     if (threadIdx.x < 8) reinterpret_cast<unsigned*>(hdr)[threadIdx.x] = 0;
-    // the tail V[K, d) starts as float(w_in) (wf32_init_kernel, launched before this kernel)
+    if constexpr (F64 && TAIL) {
+        // the tail V[K, d) starts as w_in; the chain's gathers (sc1, through L2) must see it
+        for (int i = K + threadIdx.x; i < d; i += blockDim.x) V[i] = as_global(L.w_in)[i];
+        __threadfence();
+    }
+    // (fp32: the tail V[K, d) starts as float(w_in), wf32_init_kernel launched before this kernel)
     __syncthreads();
 
     uint64_t st_wait = 0;                     // diagnostic (PSGD_STAMPS): cycles spent waiting
@@ -248,16 +292,16 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
                 const int64_t u = u0 + q;
                 if (good && u < n_fill) {
                     good = wait_for(done, &hdr->done, u - SR + SK + 1, 16);
-                    LdsSlot& sl = slots[u & (SR - 1)];
+                    LdsSlot<T>& sl = slots[u & (SR - 1)];
                     sl.col[lane] = G.ca[q];
                     sl.col[lane + 64] = G.cb[q];
-                    sl.val[lane] = float(G.xa[q]);
-                    sl.val[lane + 64] = float(G.xb[q]);
+                    sl.val[lane] = T(G.xa[q]);
+                    sl.val[lane + 64] = T(G.xb[q]);
                     if constexpr (!TAIL) {
                         // every feature in LDS: the entry's read and write address is W[j]
                         // (no tagger); inactive entries have x = 0 and use the dummy dword
-                        const unsigned ha = G.ia[q] ? kWoff + (unsigned)G.ca[q] : kLdsDummy;
-                        const unsigned hb = G.ic[q] ? kWoff + (unsigned)G.cb[q] : kLdsDummy;
+                        const unsigned ha = G.ia[q] ? kWoff + WD * (unsigned)G.ca[q] : kLdsDummy;
+                        const unsigned hb = G.ic[q] ? kWoff + WD * (unsigned)G.cb[q] : kLdsDummy;
                         sl.rw[lane] = ha | (ha << 16);
                         sl.rw[lane + 64] = hb | (hb << 16);
                         publish(&hdr->tagged, u + 1);
@@ -276,8 +320,8 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
             if (!wait_for(done, &hdr->done, g - 64, 16)) break;
             {
                 const int m = (int)((g + lane) & (kMetaRing - 1));
-                meta->y[m] = float(cur.y);
-                meta->s[m] = float(cur.s);
+                meta->y[m] = T(cur.y);
+                meta->s[m] = T(cur.s);
                 meta->s64[m] = cur.s;
                 meta->nnz[m] = (int32_t)(cur.re - cur.rb);
             }
@@ -309,7 +353,7 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
         constexpr int TB = 4;
         unsigned loaded = 0;
         uint16_t* dtag = reinterpret_cast<uint16_t*>(&hdr->dtag);
-        const int64_t chunk = ((T + kSweepRows - 1) / kSweepRows + 255) & ~int64_t(255);
+        const int64_t chunk = ((NT + kSweepRows - 1) / kSweepRows + 255) & ~int64_t(255);
         static_assert(8 % TB == 0, "n_fill is a multiple of TB");
         for (int64_t u0 = 0; u0 < n_fill; u0 += TB) {
             constexpr int nb = TB;
@@ -319,7 +363,7 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
 #pragma unroll
             for (int q = 0; q < TB; ++q) {
                 const int64_t u = u0 + q;
-                const LdsSlot& sl = slots[u & (SR - 1)];
+                const LdsSlot<T>& sl = slots[u & (SR - 1)];
                 nnz[q] = meta->nnz[u & (kMetaRing - 1)];
                 ca[q] = sl.col[lane];
                 cb[q] = sl.col[lane + 64];
@@ -346,7 +390,7 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
 #pragma unroll
                 for (int q = 0; q < TB; ++q) {
                     const int64_t lo = ((u0 + q) & (kSweepRows - 1)) * chunk;
-                    const int64_t hi = lo + chunk < T ? lo + chunk : T;
+                    const int64_t hi = lo + chunk < NT ? lo + chunk : NT;
                     si[q] = lo + 4 * lane;
                     sok[q] = si[q] < hi;
                     sv[q] = *reinterpret_cast<const uint64_t*>(tagpos + (sok[q] ? si[q] : 0));
@@ -358,7 +402,7 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
 #pragma unroll
             for (int q = 0; q < TB; ++q) {
                 const int64_t lo = ((u0 + q) & (kSweepRows - 1)) * chunk;
-                const int64_t hi = lo + chunk < T ? lo + chunk : T;
+                const int64_t hi = lo + chunk < NT ? lo + chunk : NT;
                 for (int64_t i = lo + 4 * lane; i < hi; i += 256) {
                     const uint64_t v = *reinterpret_cast<const uint64_t*>(tagpos + i);
                     *reinterpret_cast<uint64_t*>(tagpos + i) = sweep4(v);
@@ -385,15 +429,15 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
                     const bool tail = c >= K;
                     const unsigned dl = ((unsigned)u - (v >> 8)) & 255;
                     const bool prev = v != 0xFFFF && dl >= 1 && dl <= SK;
-                    const unsigned rd_tail = prev ? val_off(u - dl) + (v & 255) : kLdsDummy;
-                    const unsigned wr_tail = val_off(u) + (unsigned)e;
-                    const unsigned head = kWoff + (unsigned)c;
+                    const unsigned rd_tail = prev ? val_off(u - dl) + WD * (v & 255) : kLdsDummy;
+                    const unsigned wr_tail = val_off(u) + WD * (unsigned)e;
+                    const unsigned head = kWoff + WD * (unsigned)c;
                     const unsigned rd = e >= nnz[q] ? kLdsDummy : tail ? rd_tail : head;
                     const unsigned wr = e >= nnz[q] ? kLdsDummy : tail ? wr_tail : head;
                     return rd | (wr << 16);
                 };
                 if (q < nb) {
-                    LdsSlot& sl = slots[u & (SR - 1)];
+                    LdsSlot<T>& sl = slots[u & (SR - 1)];
                     sl.rw[lane] = rw_of(lane, ca[q], va[q]);
                     sl.rw[lane + 64] = rw_of(lane + 64, cb[q], vb[q]);
                 }
@@ -412,19 +456,20 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
     // have a consumer: the compiler treats an asm load's result as written at issue, and a dead
     // one's registers could be reused while the load is still in flight.
     double alpha = 1.0;       // SquaredL2: w = alpha * v
-    double dnsq = 0.0;        // SquaredL2: ||v||^2 - ||v_0||^2 (this lane)
+    double dnsq = 0.0;        // SquaredL2, fp32: ||v||^2 - ||v_0||^2 (this lane)
     double loss_sum = 0.0;
     float loss_blk = 0.0f;
     int64_t count = 0;
     unsigned loaded = 0, tagged = 0;
-    const i32x4 vrs = buffer_rsrc(V, (uint32_t)((int64_t)d * 4));   // the chain's vector [0, d)
+    constexpr unsigned kShift = F64 ? 3 : 2;
+    const i32x4 vrs = buffer_rsrc(reinterpret_cast<const float*>(V), (uint32_t)((int64_t)d * sizeof(T)));   // [0, d)
     auto boff = [](bool on, int32_t c) __attribute__((always_inline)) -> uint32_t {
-        return on ? (uint32_t)c << 2 : kNoAccess;
+        return on ? (uint32_t)c << kShift : kNoAccess;
     };
     // gathered tail weights: row u's in gr[u % (SK + 1)]. A gather's registers are written by
     // the load when it lands, so they are never copied before their s_waitcnt: the gather of
     // row t + SK goes to the set row t - 1 used, and the loop is unrolled SK + 1 times
-    float gr[GS][2];
+    T gr[GS][2];
     bool ok = true;
     // wait until rows < nl are loaded and rows < nt tagged (the spin path only)
     auto need = [&](int64_t nl, int64_t nt) __attribute__((always_inline)) {
@@ -438,20 +483,20 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
     // the entries of row u a gather needs
     struct GCols { int32_t c0, c1; int nnz; };
     auto gcols = [&](int64_t u) __attribute__((always_inline)) -> GCols {
-        const LdsSlot& sl = slots[u & (SR - 1)];
+        const LdsSlot<T>& sl = slots[u & (SR - 1)];
         const int nz = meta->nnz[u & (kMetaRing - 1)];
         return GCols{sl.col[lane], sl.col[lane + 64], nz};
     };
     // Only tail entries touch memory: the other lanes get the no-access offset.
-    auto gather = [&](const GCols& G, float (&g)[2]) __attribute__((always_inline)) {
+    auto gather = [&](const GCols& G, T (&g)[2]) __attribute__((always_inline)) {
         const bool a0 = lane < G.nnz && G.c0 >= K, a1 = lane + 64 < G.nnz && G.c1 >= K;
-        g[0] = buffer_gather_sc1(vrs, boff(a0, G.c0));
-        g[1] = buffer_gather_sc1(vrs, boff(a1, G.c1));
+        g[0] = buffer_gather_sc1(vrs, boff(a0, G.c0), T(0));
+        g[1] = buffer_gather_sc1(vrs, boff(a1, G.c1), T(0));
     };
     // the data of sample t
-    struct Row { float x0, x1; uint32_t rw0, rw1; int32_t c0, c1; int nnz; float y, s; double s64; };
+    struct Row { T x0, x1; uint32_t rw0, rw1; int32_t c0, c1; int nnz; T y, s; double s64; };
     auto row_of = [&](int64_t t) __attribute__((always_inline)) -> Row {
-        const LdsSlot& sl = slots[t & (SR - 1)];
+        const LdsSlot<T>& sl = slots[t & (SR - 1)];
         const int m = (int)(t & (kMetaRing - 1));
         return Row{sl.val[lane], sl.val[lane + 64], sl.rw[lane], sl.rw[lane + 64], sl.col[lane],
                    sl.col[lane + 64], meta->nnz[m], meta->y[m], meta->s[m], L2 ? meta->s64[m] : 0.0};
@@ -464,8 +509,8 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
             constexpr int q = decltype(qc)::value;
             need(q + 1, 0);
             gather(gcols(q), gr[q]);
-            buffer_store_f32(vrs, kNoAccess, 0.0f);
-            buffer_store_f32(vrs, kNoAccess, 0.0f);
+            buffer_store_f32(vrs, kNoAccess, T(0));
+            buffer_store_f32(vrs, kNoAccess, T(0));
         });
         need(SK + 1, 1);
         gc = gcols(SK);
@@ -483,7 +528,7 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
         // all issued before anything waits (the scheduling barrier keeps the compiler from
         // sinking the prefetch below the arithmetic), so their LDS round trips overlap
         const unsigned r0 = cur.rw0 & 0xFFFF, r1 = cur.rw1 & 0xFFFF;
-        const float l0 = lds[r0], l1 = lds[r1];
+        const T l0 = ld_w(r0), l1 = ld_w(r1);
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (TAIL) {
             gather(gc, gr[QN]);
@@ -491,7 +536,7 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
         }
         const Row nxt = row_of(t + 1);
         __builtin_amdgcn_sched_barrier(0);
-        float w0 = l0, w1 = l1;
+        T w0 = l0, w1 = l1;
         if constexpr (TAIL) {
             // row t's gather: issued SK samples ago, followed by 4 SK VMEM instructions
             // (PSGD_STAMPS: the time this wait takes is the chain's "wait" counter)
@@ -503,25 +548,36 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
             w0 = r0 == kLdsDummy ? gr[Q][0] : l0;
             w1 = r1 == kLdsDummy ? gr[Q][1] : l1;
         }
-        w0 = lane < cur.nnz ? w0 : 0.0f;
-        w1 = lane + 64 < cur.nnz ? w1 : 0.0f;
-        float acc = cur.x0 * w0;
-        acc = __builtin_fmaf(cur.x1, w1, acc);
-        float z = wave_sum_uniform(acc);
+        w0 = lane < cur.nnz ? w0 : T(0);
+        w1 = lane + 64 < cur.nnz ? w1 : T(0);
+        T acc = cur.x0 * w0;
+        acc = m_fma(cur.x1, w1, acc);
+        T z = wave_sum_uniform(acc);
         if constexpr (L2) {
-            z = float(alpha * double(z));
+            // w = alpha v: the dot is alpha (x . v); then the L2 shrink alpha *= 1 - s lambda
+            // (SGDUpdater.scala:176) and the step adds c x_j / alpha to v
+            z = T(alpha * double(z));
             alpha *= 1.0 - cur.s64 * kp.reg;
         }
-        float loss;
-        const float c = sparse_coef<GRAD>(z, cur.y, cur.s, loss);
-        loss_blk += t < n ? loss : 0.0f;
-        if ((t & 31) == 31) { loss_sum += double(loss_blk); loss_blk = 0.0f; }
-        const float cv = L2 ? float(double(c) / alpha) : c;
-        const float nv0 = __builtin_fmaf(cv, cur.x0, w0);
-        const float nv1 = __builtin_fmaf(cv, cur.x1, w1);
-        if constexpr (L2) dnsq += nsq_delta(w0, nv0) + nsq_delta(w1, nv1);
-        lds[cur.rw0 >> 16] = nv0;
-        lds[cur.rw1 >> 16] = nv1;
+        T c;
+        if constexpr (F64) {
+            // [ext] MLlib 1.6.1 Gradient.compute in Double (the loss included); c = -s * mult
+            double mult;
+            const double loss = gradient_scalar<GRAD, double>(z, cur.y, mult);
+            c = -cur.s * mult;
+            loss_sum += t < n ? loss : 0.0;
+        } else {
+            float loss;
+            c = sparse_coef<GRAD>(z, cur.y, cur.s, loss);
+            loss_blk += t < n ? loss : 0.0f;
+            if ((t & 31) == 31) { loss_sum += double(loss_blk); loss_blk = 0.0f; }
+        }
+        const T cv = L2 ? T(double(c) / alpha) : c;
+        const T nv0 = m_fma(cv, cur.x0, w0);
+        const T nv1 = m_fma(cv, cur.x1, w1);
+        if constexpr (L2 && !F64) dnsq += nsq_delta(w0, nv0) + nsq_delta(w1, nv1);
+        st_w(cur.rw0 >> 16, nv0);
+        st_w(cur.rw1 >> 16, nv1);
         // this row's tail stores (2 VMEM instructions)
         if constexpr (TAIL) {
             const bool a0 = lane < cur.nnz && cur.c0 >= K, a1 = lane + 64 < cur.nnz && cur.c1 >= K;
@@ -541,46 +597,96 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
     for (int q = 0; q < GS; ++q) asm volatile("" : : "v"(gr[q][0]), "v"(gr[q][1]));
     stamp_out(0);
     loss_sum += double(loss_blk);
-    if constexpr (GRAD == G_LEAST_SQUARES) loss_sum = loss_sum / 2.0;
-    // the LDS head joins the tail in L.wf32 (the fold reads w = alpha v from there); regVal
-    // of the chain's last update (PSGD.scala:257) from the tracked ||v||^2
-    for (int i = lane; i < K; i += 64) V[i] = W[i];
-    sparse_chain_out<L2>(L, kp, chain, lane, alpha, dnsq, loss_sum, count);
+    if constexpr (GRAD == G_LEAST_SQUARES && !F64) loss_sum = loss_sum / 2.0;
+    if constexpr (F64) {
+        // w = alpha v into the chain's row of L.w_out (the f64 fold), regVal of the chain's last
+        // update (PSGD.scala:257) from ||w||: the head from LDS, the tail from V (this wave's
+        // own stores, landed above; read through L2 like its gathers)
+        double* wo = L.w_out + (int64_t)chain * d;
+        double nsq = 0.0;
+        for (int i = lane; i < K; i += 64) {
+            const double wv = L2 ? alpha * W[i] : W[i];
+            wo[i] = wv;
+            if constexpr (L2) nsq += wv * wv;
+        }
+        if constexpr (TAIL) {
+            // 8 loads in flight per lane (out-of-range lanes: the no-access offset, read as 0)
+            for (int i0 = K; i0 < d; i0 += 8 * 64) {
+                double vv[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int i = i0 + q * 64 + lane;
+                    vv[q] = buffer_gather_sc1(vrs, i < d ? (uint32_t)i << 3 : kNoAccess, 0.0);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" : "+v"(vv[0]), "+v"(vv[1]), "+v"(vv[2]), "+v"(vv[3]),
+                             "+v"(vv[4]), "+v"(vv[5]), "+v"(vv[6]), "+v"(vv[7]) : : "memory");
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int i = i0 + q * 64 + lane;
+                    if (i < d) {
+                        const double wv = L2 ? alpha * vv[q] : vv[q];
+                        wo[i] = wv;
+                        if constexpr (L2) nsq += wv * wv;
+                    }
+                }
+            }
+        }
+        double rv = 0.0;
+        if constexpr (L2) {
+            nsq = wave_sum(nsq);
+            if (count > 0) {
+                const double nrm = sqrt(nsq);
+                rv = 0.5 * kp.reg * nrm * nrm;
+            }
+        }
+        if (lane == 0) {
+            L.rv[chain] = rv;
+            L.loss[chain] = loss_sum;
+            L.cnt[chain] = count;
+            L.cnt_d[chain] = double(count);
+        }
+    } else {
+        // the LDS head joins the tail in L.wf32 (the fold reads w = alpha v from there); regVal
+        // of the chain's last update (PSGD.scala:257) from the tracked ||v||^2
+        for (int i = lane; i < K; i += 64) V[i] = W[i];
+        sparse_chain_out<L2>(L, kp, chain, lane, alpha, dnsq, loss_sum, count);
+    }
 }
 
-template <typename S, int GRAD, int SK>
+template <typename S, typename T, int GRAD, int SK>
 static int lds_upd(const ChainLaunch& L, const KParams& kp, int upd, int K, size_t lds, hipStream_t st) {
-    auto k = K < kp.d ? (upd == U_SIMPLE ? chain_sparse_lds<S, GRAD, U_SIMPLE, SK, true>
-                                         : chain_sparse_lds<S, GRAD, U_SQUARED_L2, SK, true>)
-                      : (upd == U_SIMPLE ? chain_sparse_lds<S, GRAD, U_SIMPLE, SK, false>
-                                         : chain_sparse_lds<S, GRAD, U_SQUARED_L2, SK, false>);
+    auto k = K < kp.d ? (upd == U_SIMPLE ? chain_sparse_lds<S, T, GRAD, U_SIMPLE, SK, true>
+                                         : chain_sparse_lds<S, T, GRAD, U_SQUARED_L2, SK, true>)
+                      : (upd == U_SIMPLE ? chain_sparse_lds<S, T, GRAD, U_SIMPLE, SK, false>
+                                         : chain_sparse_lds<S, T, GRAD, U_SQUARED_L2, SK, false>);
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(192), lds, st, L, kp, K);
     return (int)hipGetLastError();
 }
 
-template <typename S, int SK>
+template <typename S, typename T, int SK>
 static int lds_grad(const ChainLaunch& L, const KParams& kp, int grad, int upd, int K, size_t lds, hipStream_t st) {
     switch (grad) {
-    case G_LOGISTIC: return lds_upd<S, G_LOGISTIC, SK>(L, kp, upd, K, lds, st);
-    case G_LEAST_SQUARES: return lds_upd<S, G_LEAST_SQUARES, SK>(L, kp, upd, K, lds, st);
-    case G_HINGE: return lds_upd<S, G_HINGE, SK>(L, kp, upd, K, lds, st);
+    case G_LOGISTIC: return lds_upd<S, T, G_LOGISTIC, SK>(L, kp, upd, K, lds, st);
+    case G_LEAST_SQUARES: return lds_upd<S, T, G_LEAST_SQUARES, SK>(L, kp, upd, K, lds, st);
+    case G_HINGE: return lds_upd<S, T, G_HINGE, SK>(L, kp, upd, K, lds, st);
     default: return -3;
     }
 }
 
-template <int SK>
+// Variant 600 + 10 (SK == 8) + 20 (fp64 compute) + storage (1: f32 rows).
+template <int SK, typename T>
 static int lds_launch(const ChainLaunch& L, const KParams& kp, int storage, int gradient, int updater,
                       hipStream_t stream, int* kernel_variant) {
-    int64_t K = lds_head<SK>(kp.d);
+    int64_t K = lds_head<SK, T>(kp.d);
     if (K < 0) return -3;
     // tests: PSGD_SPARSE_LDS_HEAD=k caps the LDS-resident head (exercises the tail at small d)
     if (const char* e = getenv("PSGD_SPARSE_LDS_HEAD"))
         if (*e) { const int64_t cap = atoll(e) & ~int64_t(3); if (cap >= 0 && cap < K) K = cap; }
-    const size_t lds = (size_t)lds_bytes<SK>(kp.d, K);
-    if (kernel_variant) *kernel_variant = 600 + (SK == 8 ? 10 : 0) + storage;
-    if (storage == 1) return lds_grad<float, SK>(L, kp, gradient, updater, (int)K, lds, stream);
-    return lds_grad<double, SK>(L, kp, gradient, updater, (int)K, lds, stream);
+    const size_t lds = (size_t)lds_bytes<SK, T>(kp.d, K);
+    if (kernel_variant) *kernel_variant = 600 + (SK == 8 ? 10 : 0) + (sizeof(T) == 8 ? 20 : 0) + storage;
+    if (storage == 1) return lds_grad<float, T, SK>(L, kp, gradient, updater, (int)K, lds, stream);
+    return lds_grad<double, T, SK>(L, kp, gradient, updater, (int)K, lds, stream);
 }
 
 // Speculation depth: 4 rows by default (tail gathers are L2 hits once the tails fit L2);
@@ -592,18 +698,35 @@ static int lds_depth() {
 
 bool sparse_lds_applies(int64_t d, int64_t max_nnz) {
     if (max_nnz > LCAP) return false;
-    return (lds_depth() == 8 ? lds_head<8>(d) : lds_head<4>(d)) >= 0;
+    return (lds_depth() == 8 ? lds_head<8, float>(d) : lds_head<4, float>(d)) >= 0;
 }
 
-int64_t sparse_lds_head(int64_t d) { return lds_depth() == 8 ? lds_head<8>(d) : lds_head<4>(d); }
+int64_t sparse_lds_head(int64_t d) { return lds_depth() == 8 ? lds_head<8, float>(d) : lds_head<4, float>(d); }
 
 int launch_sparse_lds_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
                              int updater, int64_t max_nnz, hipStream_t stream, int* kernel_variant) {
     if (kp.n_chains <= 0) return 0;
     if (!sparse_lds_applies(kp.d, max_nnz)) return -3;
     if (!L.wf32 || L.wstride < (int64_t)kp.d + 128 + 1024) return (int)hipErrorInvalidValue;
-    if (lds_depth() == 8) return lds_launch<8>(L, kp, storage, gradient, updater, stream, kernel_variant);
-    return lds_launch<4>(L, kp, storage, gradient, updater, stream, kernel_variant);
+    if (lds_depth() == 8) return lds_launch<8, float>(L, kp, storage, gradient, updater, stream, kernel_variant);
+    return lds_launch<4, float>(L, kp, storage, gradient, updater, stream, kernel_variant);
+}
+
+bool sparse_lds64_applies(int64_t d, int64_t max_nnz, int updater, bool check_conv, bool alpha_ok) {
+    if (max_nnz > LCAP || check_conv) return false;
+    if (updater != U_SIMPLE && !(updater == U_SQUARED_L2 && alpha_ok)) return false;
+    return (lds_depth() == 8 ? lds_head<8, double>(d) : lds_head<4, double>(d)) >= 0;
+}
+
+int launch_sparse_lds64_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
+                               int updater, int64_t max_nnz, hipStream_t stream, int* kernel_variant) {
+    if (kp.n_chains <= 0) return 0;
+    if (!sparse_lds64_applies(kp.d, max_nnz, updater, false, kp.alpha_ok != 0)) return -3;
+    // the chain's f64 vector: [d] + [128] + [1024] doubles inside its slice of L.wf32
+    if (!L.wf32 || L.wstride < 2 * ((int64_t)kp.d + 128 + 1024) || (L.wstride & 3) || !L.w_out)
+        return (int)hipErrorInvalidValue;
+    if (lds_depth() == 8) return lds_launch<8, double>(L, kp, storage, gradient, updater, stream, kernel_variant);
+    return lds_launch<4, double>(L, kp, storage, gradient, updater, stream, kernel_variant);
 }
 
 }  // namespace psgd

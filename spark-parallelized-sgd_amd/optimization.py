@@ -123,13 +123,19 @@ class ShardedEngine:
             partial, counts = self.empty_partial(w), None
         if self.world == 1:
             return partial, counts
+        return self.exchange(partial), counts
+
+    def exchange(self, partial):
+        """The cross-process level of the treeReduce: all-gather every rank's (d+3) partial
+        (RCCL over xGMI with the nccl backend; gloo's list form on CPU) and fold them in rank
+        order with the reference's combiner (ParallelizedSGD.scala:271-276)."""
         import torch.distributed as dist
         out = self.gather_buffer()
         if dist.get_backend() == "gloo":
             dist.all_gather(list(out.view(self.world, self.d + 3).unbind(0)), partial)
         else:
             dist.all_gather_into_tensor(out, partial)
-        return self.fold_partials(out), counts
+        return self.fold_partials(out)
 
 
 class HipEngine(ShardedEngine):

@@ -5,7 +5,7 @@
 * C4 (Hinge CSR, rcv1-like: d = 47,236, 60-128 nnz/row, rows L2-normalised) on 256 chains:
   fp32 through chain_sparse_lds (variant 601: an LDS head of ~22k features, the tail in HBM) and
   chain_sparse_spec (variant 411, its 94 KB LDS tag table at this d), and fp64
-  through chain_general (variant 201).
+  through chain_sparse_lds in fp64 (variant 620: an LDS head of ~5k doubles, the tail in HBM).
 * C5 (L2 Logistic CSR, d = 2^22, 100 nnz/row, lambda 1e-6, step 0.5): fp32 chain_sparse
   (variant 401, HBM-resident weights) and fp64 chain_general's alpha-scaled lazy SquaredL2.
 * psgd_fold_partials_device (the cross-GPU level of the treeReduce, PSGD.scala:271-276) bit for
@@ -145,7 +145,7 @@ def test_c4_rcv1_shape_fp64(pkg, oracle, c4):
     data = csr_parts(pkg, y, rp, col, val, d, offs)
     w, h, counts = pkg.runParallelizedSGD(data, pkg.HingeGradient(), pkg.SimpleSGDUpdater(), 1.0, 2, 0.0, 1.0,
                                           np.zeros(d), 0.0, return_chain_counts=True)
-    assert pkg.optimization.get_context(0).last_kernel() == 201   # chain_general, CSR
+    assert pkg.optimization.get_context(0).last_kernel() == 620   # chain_sparse_lds<double, double>
     mat = oracle.Matrix(y, row_ptr=rp, col=col, val=val, d=d)
     wr, hr, cr = oracle.run(mat, offs, "hinge", "simple", 1.0, 2, 0.0, np.zeros(d), tol=0.0, n_threads=8)
     assert [list(map(int, c)) for c in counts] == [list(map(int, c)) for c in cr]
@@ -305,3 +305,58 @@ def test_hip_engine_two_ranks(tmp_path, pkg, oracle, P):
     assert [list(c) for c in c0] == [list(c[:lo1]) for c in cr[: len(c0)]]
     if P > 1:
         assert [list(c) for c in c1] == [list(c[lo1:]) for c in cr[: len(c1)]]
+
+
+def test_rccl_exchange_single_rank(tmp_path):
+    """The engine's RCCL leg (ShardedEngine.exchange: dist.all_gather_into_tensor into the gather
+    buffer, then psgd_fold_partials_device) in a one-rank nccl process group: bit for bit the
+    single-process epoch's partial, for dense fp64 and CSR fp32 partitions."""
+    out = str(tmp_path / "rccl.npz")
+    script = os.path.join(ROOT, "tests", "one_rank_nccl.py")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    r = subprocess.run([sys.executable, script, out], env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = np.load(out)
+    for name in ("dense", "csr"):
+        single, rccl = res[name + "_single"], res[name + "_rccl"]
+        assert np.isfinite(single).all() and single[-1] > 0, name
+        assert np.array_equal(single, rccl), name
+
+
+@pytest.fixture(scope="module")
+def c5_full_chains(oracle):
+    """C5's per-GPU geometry: 1,024 chains over d = 2^22 (1,024 f32 weight vectors = 17 GB of
+    wf32 in the fp32 mode), 2-4 rows each (ragged), 100 nnz per row; f32-representable values,
+    so that one oracle run (2 iterations, ~1 min on 16 threads) serves both compute modes."""
+    rng = np.random.default_rng(5050)
+    d, P = 1 << 22, 1024
+    per = rng.integers(2, 5, size=P)
+    offs = [0] + [int(o) for o in np.cumsum(per)]
+    n = offs[-1]
+    rp, col, val = csr_rows(rng, n, d, 100, 100, normal_vals=True)
+    val = val.astype(np.float32).astype(np.float64)
+    y = planted_labels(rng, rp, col, val, d)
+    mat = oracle.Matrix(y, row_ptr=rp, col=col, val=val, d=d)
+    ref = oracle.run(mat, offs, "logistic", "squared_l2", 0.5, 2, 1e-6, np.zeros(d), tol=0.0, n_threads=16)
+    return d, rp, col, val, y, offs, ref
+
+
+@pytest.mark.parametrize("compute,want", [("f32", 401), ("f64", 201)])
+def test_c5_1024_chains(pkg, c5_full_chains, compute, want):
+    """C5 at its real chain count: wf32_init_kernel over 1,024 chains x 2^22 features, the
+    chains, fold_f32_kernel over 1,024 fp32 vectors (f32); chain_general's alpha-scaled lazy
+    SquaredL2 and fold_kernel over 1,024 f64 vectors (f64). Against the oracle: counts exact,
+    fp64 at 1e-9, fp32 at its stated tolerance."""
+    d, rp, col, val, y, offs, (wr, hr, cr) = c5_full_chains
+    vs = val.astype(np.float32) if compute == "f32" else val
+    data = csr_parts(pkg, y, rp, col, vs, d, offs)
+    w, h, counts = pkg.runParallelizedSGD(data, pkg.LogisticGradient(), pkg.SquaredL2SGDUpdater(), 0.5, 2,
+                                          1e-6, 1.0, np.zeros(d), 0.0, compute_dtype=compute,
+                                          return_chain_counts=True)
+    assert pkg.optimization.get_context(0).last_kernel() == want
+    assert [list(map(int, c)) for c in counts] == [list(map(int, c)) for c in cr]
+    if compute == "f32":
+        check_fp32(w, h, wr, hr, "c5 1024 chains fp32")
+    else:
+        assert_close(w, wr, what="c5 1024 chains fp64 weights")
+        assert_close(h, hr, what="c5 1024 chains fp64 loss")

@@ -253,6 +253,16 @@ def test_csr_stateful_updater(pkg, oracle):
         assert_close(h, hr, what=upd + " loss")
 
 
+def alpha_in_range(step, reg, n):
+    """The host's test for the fp64 CSR kernel's alpha-scaled form (psgd_capi.cpp alpha_in_range)."""
+    a = 1.0
+    for j in range(1, n + 1):
+        a *= 1.0 - (step / np.sqrt(float(j))) * reg
+        if not (2.0 ** -400 <= abs(a) <= 2.0 ** 400):
+            return False
+    return True
+
+
 @pytest.mark.parametrize("reg,step", [(0.01, 0.5), (0.999, 1.0), (1.0, 1.0), (3.0, 1.0), (1e-6, 0.5)])
 def test_csr_squared_l2_alpha_scaled(pkg, oracle, reg, step):
     """fp64 CSR SquaredL2 without a convergence test keeps w = alpha * v (O(nnz) per sample):
@@ -277,7 +287,9 @@ def test_csr_squared_l2_alpha_scaled(pkg, oracle, reg, step):
         w, h, counts = pkg.runParallelizedSGD(pkg.PartitionedData(parts), getattr(pkg, G[grad])(),
                                               pkg.SquaredL2SGDUpdater(), step, 3, reg, 1.0, w0, 0.0,
                                               return_chain_counts=True)
-        assert pkg.optimization.get_context(0).last_kernel() == 201
+        # chain_sparse_lds in fp64 (62x) while every prefix product of (1 - s_j lambda) stays in
+        # [2^-400, 2^400]; else chain_general (201), which renormalises
+        assert pkg.optimization.get_context(0).last_kernel() == (620 if alpha_in_range(step, reg, 700) else 201)
         wr, hr, cr = oracle.run(oracle.Matrix(y, row_ptr=rp, col=col, val=val, d=d), offs, grad, "squared_l2",
                                 step, 3, reg, w0, tol=0.0)
         assert [list(map(int, c)) for c in counts] == [list(map(int, c)) for c in cr]
@@ -468,3 +480,32 @@ def test_fp64_block_rows_in_registers(pkg, oracle, d, grad, upd, storage):
     assert [list(c) for c in counts] == [list(c) for c in cr[: len(counts)]]
     assert_close(w, wr, what=f"d={d} {grad} {upd} weights")
     assert_close(h, hr, what=f"d={d} {grad} {upd} loss")
+
+
+@pytest.mark.parametrize("upd", ["adagrad", "adam"])
+@pytest.mark.parametrize("d,storage", [(40, np.float64), (300, np.float32), (1024, np.float32),
+                                       (1024, np.float64)])
+def test_dense_fp64_stateful_updaters_in_registers(pkg, oracle, upd, d, storage):
+    """AdaGrad / Adam (SGDUpdater.scala:193-286) in the fp64 parity mode on chain_dense: the
+    weights and the updater status in registers (variant 10x, d <= 1,024), f32 and f64 rows,
+    tol 0 and tol > 0 (per-sample breaks). 1e-9 and exact counts against the oracle."""
+    rng = np.random.default_rng(d * 3 + len(upd))
+    n, P = 2400, 4
+    X, y = synth(rng, n, d, "logistic", np.float32)
+    data = pkg.PartitionedData.parallelize(y, X.astype(storage), P, dtype=storage)
+    offs = [i * n // P for i in range(P)] + [n]
+    step = 0.05
+    vec = 4 if storage == np.float32 else 2
+    nv = 1
+    while nv * 64 * vec < d:
+        nv *= 2
+    for tol in (0.0, 0.001):
+        w, h, counts = pkg.runParallelizedSGD(data, pkg.LogisticGradient(), getattr(pkg, U[upd])(), step, 3,
+                                              0.0, 1.0, np.zeros(d), tol, return_chain_counts=True)
+        assert pkg.optimization.get_context(0).last_kernel() == 100 + nv
+        wr, hr, cr = oracle.run(oracle.Matrix(y, X.astype(np.float64)), offs, "logistic", upd, step, 3, 0.0,
+                                np.zeros(d), tol=tol, n_threads=8)
+        tag = f"{upd} d={d} {np.dtype(storage).name} tol={tol}"
+        assert [list(c) for c in counts] == [list(c) for c in cr[: len(counts)]], tag
+        assert_close(w, wr, what=tag + " weights")
+        assert_close(h, hr, what=tag + " loss")

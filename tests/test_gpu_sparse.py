@@ -169,3 +169,89 @@ def test_sparse_device_registration(pkg, oracle):
     wr, hr, _ = oracle.run(mat, offs, "least_squares", "simple", 0.3, 3, 0.0, np.zeros(d), tol=0.0)
     assert np.max(np.abs(w - wr)) <= FP32_REL * np.max(np.abs(wr))
     assert np.max(np.abs(h - hr) / np.abs(hr)) <= FP32_LOSS_REL
+
+
+# ------------------------------------------------------------------------------------------
+# fp64 compute (the parity mode) on chain_sparse_lds<., double>: 1e-9 and exact counts.
+# ------------------------------------------------------------------------------------------
+KERNELS64 = {  # name: (environment, variant base without the storage digit)
+    "lds64": ({}, 620),
+    "lds64_tail": ({"PSGD_SPARSE_LDS_HEAD": "third"}, 620),
+    "lds64_tail_sk8": ({"PSGD_SPARSE_LDS_HEAD": "third", "PSGD_SPARSE_SK": "8"}, 630),
+}
+
+
+@pytest.fixture(params=sorted(KERNELS64))
+def kernel64(request, monkeypatch):
+    env, base = KERNELS64[request.param]
+    for k in ("PSGD_SPARSE_KERNEL", "PSGD_SPARSE_LDS_HEAD", "PSGD_SPARSE_SK"):
+        monkeypatch.delenv(k, raising=False)
+
+    def apply(d):
+        for k, v in env.items():
+            monkeypatch.setenv(k, str(max(d // 3, 0)) if v == "third" else v)
+        return base
+    return apply
+
+
+def check64(pkg, oracle, rp, col, val, y, d, offs, grad, upd, step, reg, iters, frac=1.0, dtype=np.float64,
+            kernel=None, want=None):
+    from test_gpu_parity import assert_close
+    base = kernel(d) if kernel else 620
+    vstore = val.astype(dtype)
+    parts = [pkg.CsrPartition(y[a:b], rp[a:b + 1] - rp[a], col[rp[a]:rp[b]], vstore[rp[a]:rp[b]], d)
+             for a, b in zip(offs[:-1], offs[1:])]
+    w, h, counts = pkg.runParallelizedSGD(pkg.PartitionedData(parts), getattr(pkg, G[grad])(),
+                                          getattr(pkg, U[upd])(), step, iters, reg, frac, np.zeros(d), 0.0,
+                                          return_chain_counts=True)
+    if want is None:
+        wide = int(np.max(np.diff(rp))) > 128
+        want = 201 if wide else base + (1 if dtype == np.float32 else 0)
+    assert pkg.optimization.get_context(0).last_kernel() == want
+    mat = oracle.Matrix(y, row_ptr=rp, col=col, val=vstore.astype(np.float64), d=d)
+    wr, hr, cr = oracle.run(mat, offs, grad, upd, step, iters, reg, np.zeros(d), tol=0.0, fraction=frac,
+                            n_threads=8)
+    tag = f"fp64 d={d} {grad} {upd} f={frac}"
+    assert [list(c) for c in counts] == [list(c) for c in cr[: len(counts)]], tag
+    assert_close(w, wr, what=tag + " weights")
+    assert_close(h, hr, what=tag + " loss")
+
+
+@pytest.mark.parametrize("grad", ["least_squares", "logistic", "hinge"])
+@pytest.mark.parametrize("upd", ["simple", "squared_l2"])
+def test_sparse_fp64_wide(pkg, oracle, grad, upd, kernel64):
+    rng = np.random.default_rng(len(grad) * 11 + len(upd))
+    n, d = 1500, 3000
+    rp, col, val, y = synth_csr(rng, n, d, 0, 40, grad)
+    offs = [0, 500, 500, 501, 1500]
+    check64(pkg, oracle, rp, col, val, y, d, offs, grad, upd, 0.3, 0.05, 3, kernel=kernel64)
+
+
+@pytest.mark.parametrize("grad", ["least_squares", "logistic", "hinge"])
+def test_sparse_fp64_narrow_overlapping_rows(pkg, oracle, grad, kernel64):
+    rng = np.random.default_rng(23 + len(grad))
+    n, d = 900, 12
+    rp, col, val, y = synth_csr(rng, n, d, 1, 9, grad)
+    offs = [0, 300, 600, 900]
+    check64(pkg, oracle, rp, col, val, y, d, offs, grad, "simple", 0.2, 0.0, 3, kernel=kernel64)
+    check64(pkg, oracle, rp, col, val, y, d, offs, grad, "squared_l2", 0.2, 0.1, 2, kernel=kernel64)
+
+
+def test_sparse_fp64_f32_rows_and_sampled_batches(pkg, oracle, kernel64):
+    rng = np.random.default_rng(24)
+    n, d = 2000, 500
+    rp, col, val, y = synth_csr(rng, n, d, 0, 30, "hinge")
+    check64(pkg, oracle, rp, col, val, y, d, [0, 1000, 2000], "hinge", "squared_l2", 0.5, 0.01, 2,
+            dtype=np.float32, kernel=kernel64)
+    for frac in (0.15, 0.6):
+        check64(pkg, oracle, rp, col, val, y, d, [0, 1000, 2000], "hinge", "simple", 0.5, 0.0, 3, frac=frac,
+                kernel=kernel64)
+
+
+def test_sparse_fp64_alpha_out_of_range_takes_chain_general(pkg, oracle):
+    """SquaredL2 with 1 - s*lambda = 0 at the first sample (alpha = 0): the alpha-scaled form
+    without renormalisation does not apply, chain_general (which renormalises) runs."""
+    rng = np.random.default_rng(25)
+    n, d = 600, 300
+    rp, col, val, y = synth_csr(rng, n, d, 1, 20, "logistic")
+    check64(pkg, oracle, rp, col, val, y, d, [0, 300, 600], "logistic", "squared_l2", 1.0, 1.0, 2, want=201)
