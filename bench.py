@@ -45,8 +45,8 @@ SECONDARY_ROWS = {"c5": 20_000_000}
 # reference's own Double rows (8,200 B per sample)
 # (AdaGrad / Adam on the logistic c3 shard: the reference's Adam, r^iter in fix1 (UPD.scala:262),
 # turns NaN once the squared-gradient average r exceeds 1, which least squares at c2 reaches)
-DEFAULT_SECONDARY = ("c3:f64,c3:f64::f64,c3:f32,c2:f64,c1:f64,c4:f32,c5:f32,"
-                     "c3:f32:adagrad,c3:f32:adam")
+DEFAULT_SECONDARY = ("c3:f64::f64,c3:f64,c3:f32,c2:f64,c1:f64,c4:f32,c4:f64,c5:f32,"
+                     "c3:f32:adagrad,c3:f32:adam,c3:f64:adagrad,c3:f64:adam")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
@@ -58,15 +58,18 @@ def pmc_traffic(workload, grad, variant, storage, rows, compute="f32", updater="
     import glob
     files = glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_pmc.json")) + \
         glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_*_pmc.json"))
-    if not files or not (300 <= variant < 800):
+    if not files or not (100 <= variant < 200 or 300 <= variant < 800):
         return None, None
     waves = 0
     g = {"logistic": 0, "least_squares": 1, "hinge": 2}[grad]
-    u = {"simple": 0, "squared_l2": 1}.get(updater)
+    u = {"simple": 0, "squared_l2": 1, "l1": 2, "adagrad": 3, "adam": 4}.get(updater)
     if u is None:
         return None, None
     sname = "float" if storage == "f32" else "double"
-    if variant >= 700:
+    if variant < 200:   # chain_dense<S, T, GRAD, UPD, CONV = false, NV, FULL>
+        cname = "float" if compute == "f32" else "double"
+        prefix = f"psgd::chain_dense<{sname}, {cname}, {g}, {u}, false, {variant - 100},"
+    elif variant >= 700:
         prefix = f"psgd::chain_block64<{sname}, {g}, {u}, {variant % 10}, "
         waves = 1 + (variant - 700) // 10
     elif variant >= 600:
@@ -392,8 +395,13 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
     variant = engine.ctx.last_kernel()
     upd_name = updater or ("squared_l2" if reg > 0 else "simple")
     traffic, traffic_src = pmc_traffic(workload, grad, variant, sdt, n, compute, upd_name)
+    note = None
+    if compute == "f32" and workload == "c3" and not updater:
+        note = ("fp32 compute at C3's step 1.0 is a throughput mode without a uniform weight tolerance "
+                "(DESIGN.md §4); the parity claims for C3 are the fp64 lines")
     res = {
         "value": value, "ms_per_step": elapsed / steps * 1e3, "dtype": compute, "loss": loss,
+        **({"precision_note": note} if note else {}),
         "config": {"workload": f"{workload}: {cfg_name}", "rows_per_gpu": n, "d": d,
                    "chains_per_gpu": P, "storage": sdt, "gradient": grad,
                    "updater": updater or ("squared_l2" if reg > 0 else "simple"), "reg_param": reg,

@@ -25,6 +25,29 @@
 
 namespace psgd {
 
+// 1/sqrt(x) for x >= 1 in f64: v_rsq_f64 and two Newton steps (x = inf gives 0, NaN stays NaN).
+__device__ __forceinline__ double rsqrt_newton(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const double e = __builtin_fma(-(x * y), y, 1.0);
+        y = __builtin_fma(0.5 * y, e, y);
+    }
+    return x == __builtin_inf() ? 0.0 : y;
+}
+
+// pow(r, iter) of AdamSGDUpdater's fix1 (UPD.scala:262) for iter = j >= 1: when iter * log2(r) <
+// -1100 the power is below 2^-1100 and the library pow returns 0 (it rounds below half the
+// least denormal); the hardware f32 log2 (relative error ~1e-7, so the margin to 2^-1075 is
+// ~25 binades) decides that without the ~100-instruction f64 pow, which after a few hundred
+// samples no coordinate needs (r is an average of squared gradients, well below 1).
+__device__ __forceinline__ double pow_int_iter(double r, double iter) {
+    const float l2 = __builtin_amdgcn_logf((float)r);
+    double p = 0.0;
+    if (!((float)iter * l2 < -1100.0f)) p = pow(r, iter);
+    return p;
+}
+
 template <typename S, typename T, int GRAD, int UPD, bool CONV, int NV, bool FULL>
 __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, RingGeom geom) {
     using V = typename Vec16<S>::type;
@@ -233,9 +256,11 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, Ri
                     nw.x = old.x + a * (g.x * __builtin_amdgcn_rsqf(acc2.x + T(1)));
                     nw.y = old.y + a * (g.y * __builtin_amdgcn_rsqf(acc2.y + T(1)));
                 } else {
-                    // pow(accum + 1.0, 0.5) as the correctly rounded sqrt (UPD.scala:209)
-                    nw.x = old.x + a * (g.x / m_sqrt(acc2.x + T(1)));
-                    nw.y = old.y + a * (g.y / m_sqrt(acc2.y + T(1)));
+                    // g / pow(accum + 1.0, 0.5) (UPD.scala:209) as g * rsqrt(accum + 1): v_rsq_f64
+                    // and two Newton steps (within ~2 ulp; the library sqrt + division were
+                    // ~20 dependent f64 operations per coordinate and sample)
+                    nw.x = old.x + a * (g.x * rsqrt_newton(acc2.x + T(1)));
+                    nw.y = old.y + a * (g.y * rsqrt_newton(acc2.y + T(1)));
                 }
             } else if constexpr (UPD == U_ADAM) {
                 // the reference's variant, literally: v = beta v + (1-beta) g,
@@ -258,8 +283,8 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, Ri
                     nw.x = old.x + al * (v.x * __builtin_amdgcn_rcpf(fx));
                     nw.y = old.y + al * (v.y * __builtin_amdgcn_rcpf(fy));
                 } else {
-                    const T fx = m_sqrt(T(1) - m_pow(r.x, iter)) + T(kp.eps);
-                    const T fy = m_sqrt(T(1) - m_pow(r.y, iter)) + T(kp.eps);
+                    const T fx = m_sqrt(T(1) - pow_int_iter(r.x, iter)) + T(kp.eps);
+                    const T fy = m_sqrt(T(1) - pow_int_iter(r.y, iter)) + T(kp.eps);
                     nw.x = old.x + al * (v.x / fx);
                     nw.y = old.y + al * (v.y / fy);
                 }
