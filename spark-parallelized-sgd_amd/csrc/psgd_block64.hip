@@ -442,7 +442,7 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
     };
     // This wave's share of a block's rows, from the ring into registers (as stored, or as
     // doubles with CONV1); rows >= kk (a tail block) are zero.
-    V xraw[kB][CONV1 ? 1 : NVH];
+    V xraw[kB][NVH];
     double xcv[CONV1 ? kB : 1][CONV1 ? EH : 1];
     auto load_rows = [&](auto tail_c, const char* base, int kk) __attribute__((always_inline)) {
         constexpr bool TAIL = decltype(tail_c)::value;
@@ -456,9 +456,17 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
                     if ((v * 64 + lane) * VEC >= dsc.ld) xv = V(0);
                 }
                 if (TAIL && k >= kk) xv = V(0);
-                if constexpr (CONV1) unpack<S, double>(xv, &xcv[k][u * VEC]);
-                else xraw[k][u] = xv;
+                xraw[k][u] = xv;
             }
+        }
+        if constexpr (CONV1) {
+            // every read is issued before the first conversion: converting as each read lands
+            // made the compiler reuse one register quad and wait for every read in turn
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < kB; ++k)
+#pragma unroll
+                for (int u = 0; u < NVH; ++u) unpack<S, double>(xraw[k][u], &xcv[k][u * VEC]);
         }
     };
     // VEC doubles of row k, slice u

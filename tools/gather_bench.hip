@@ -9,6 +9,8 @@
 //   MODE 1: gathers (sc1) only
 //   MODE 2: stores only
 //   MODE 3: gathers without sc1 + stores
+//   MODE 4: stores only, nt;  MODE 5: stores only, sc1 (cache-policy A/B of the scattered stores;
+//   run under rocprofv3 --pmc WRITE_SIZE with a small d to see whether they stay in L2)
 // DEPTH rows' gathers are in flight before the group's stores (DEPTH = 1: each row's stores
 // wait for its own gathers, the chain's dependence; deeper: independent rows, the rate a deeper
 // pipeline could reach). The best rate over the depths is the pattern's ceiling on this chip.
@@ -33,6 +35,12 @@ __device__ __forceinline__ float gather(const float* p) {
 __device__ __forceinline__ void store(float* p, float v) {
     asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");
 }
+__device__ __forceinline__ void store_nt(float* p, float v) {
+    asm volatile("global_store_dword %0, %1, off nt" : : "v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void store_sc1(float* p, float v) {
+    asm volatile("global_store_dword %0, %1, off sc1" : : "v"(p), "v"(v) : "memory");
+}
 
 template <int MODE, int DEPTH>
 __global__ __launch_bounds__(64) void gather_store(float* W, long stride, int rows, unsigned width, int nnz) {
@@ -51,7 +59,7 @@ __global__ __launch_bounds__(64) void gather_store(float* W, long stride, int ro
             const unsigned h = mix(key ^ (unsigned)(r + q) * 0x85EBCA6Bu);
             p0[q] = lane < nnz ? base + (long)lane * width + mix(h + lane) % width : dummy;
             p1[q] = lane + 64 < nnz ? base + (long)(lane + 64) * width + mix(h + lane + 64) % width : dummy;
-            if constexpr (MODE != 2) {
+            if constexpr (MODE != 2 && MODE != 4 && MODE != 5) {
                 g0[q] = gather<MODE>(p0[q]);
                 g1[q] = gather<MODE>(p1[q]);
             } else {
@@ -61,7 +69,13 @@ __global__ __launch_bounds__(64) void gather_store(float* W, long stride, int ro
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
         for (int q = 0; q < DEPTH; ++q) {
-            if constexpr (MODE != 1) {
+            if constexpr (MODE == 4) {
+                store_nt(p0[q], g0[q] + 1.0f);
+                store_nt(p1[q], g1[q] + 1.0f);
+            } else if constexpr (MODE == 5) {
+                store_sc1(p0[q], g0[q] + 1.0f);
+                store_sc1(p1[q], g1[q] + 1.0f);
+            } else if constexpr (MODE != 1) {
                 store(p0[q], g0[q] + 1.0f);
                 store(p1[q], g1[q] + 1.0f);
             }
@@ -102,7 +116,8 @@ int main(int argc, char** argv) {
     printf("gather_bench: %d chains x %d rows x %d entries, d = %u (%.1f GB of weights)\n", chains, rows, nnz,
            d, (double)chains * stride * 4 / 1e9);
     const double R = (double)rows * chains;
-    const char* names[4] = {"gather sc1 + store (c5)", "gather sc1 only", "store only", "gather plain + store"};
+    const char* names[6] = {"gather sc1 + store (c5)", "gather sc1 only", "store only", "gather plain + store",
+                            "store only (nt)", "store only (sc1)"};
     auto report = [&](int mode, int depth, float ms) {
         printf("  %-24s depth %2d: %8.3f ms  %7.1f M rows/s  %6.2f G lane-requests/s\n", names[mode], depth, ms,
                R / ms / 1e3, R * (mode == 0 || mode == 3 ? 2 : 1) * nnz / ms / 1e6);
@@ -111,6 +126,6 @@ int main(int argc, char** argv) {
     report(M, 1, run<M, 1>(W, stride, rows, chains, width, nnz)); \
     report(M, 4, run<M, 4>(W, stride, rows, chains, width, nnz)); \
     report(M, 16, run<M, 16>(W, stride, rows, chains, width, nnz));
-    RUN(0) RUN(1) RUN(2) RUN(3)
+    RUN(0) RUN(1) RUN(2) RUN(3) RUN(4) RUN(5)
     return 0;
 }
