@@ -13,7 +13,7 @@ from ._native import (DeviceError, IllegalArgumentException, UnsupportedOperatio
 from .data import (CsrPartition, DensePartition, DeviceCsrPartition, DevicePartition, PartitionedData,
                    shard_range)
 from .gradient import Gradient, HingeGradient, LeastSquaresGradient, LogisticGradient
-from .optimization import (HipEngine, ParallelizedSGD, ShardedEngine, make_params,
+from .optimization import (DriverCheckpoint, HipEngine, ParallelizedSGD, ShardedEngine, make_params,
                            runParallelizedSGD)
 from .updater import (AdaGradSGDUpdater, AdamSGDUpdater, L1SGDUpdater, SGDUpdater,
                       SimpleSGDUpdater, SquaredL2SGDUpdater)

@@ -335,9 +335,15 @@ class ParallelizedSGD:
                            stepSize: float, numIterations: int, regParam: float,
                            miniBatchFraction: float, initialWeights, convergenceTol: float = 0.001,
                            *, compute_dtype: str = "f64", engine=None,
-                           return_chain_counts: bool = False):
+                           return_chain_counts: bool = False,
+                           checkpoint: Optional[str] = None, checkpoint_every: int = 1):
         """ParallelizedSGD.scala:188-306 (and the 8-argument alias :311-321 via the default).
-        Returns (weights, stochasticLossHistory) [, per-iteration chain counts]."""
+        Returns (weights, stochasticLossHistory) [, per-iteration chain counts].
+
+        checkpoint: a file path (extension): the loop state is saved there every
+        `checkpoint_every` iterations and after the last one, and a run that finds a checkpoint of
+        the same parameters and data resumes from it (DriverCheckpoint). The chain counts of
+        iterations before the resume are not in it."""
         if miniBatchFraction < 1.0 and convergenceTol > 0.0:  # :200-203
             log.warning("Testing against a convergenceTol when using miniBatchFraction "
                         "< 1.0 can be unstable because of the stochasticity in sampling.")
@@ -369,11 +375,21 @@ class ParallelizedSGD:
 
         params = make_params(gradient, updater, stepSize, regParam, miniBatchFraction,
                              convergenceTol, compute_dtype)
-        weights = engine.weights(w0)                      # :224
-        regVal = engine.initial_regval(params, w0)        # :231-233
-        have_current = False
-        converged = False
-        i = 1
+        ckpt = DriverCheckpoint(checkpoint, checkpoint_every) if checkpoint else None
+        fp = _ckpt_fingerprint(params, data, w0) if ckpt else None
+        state = ckpt.load(fp) if ckpt else None
+        if state is None:
+            weights = engine.weights(w0)                  # :224
+            regVal = engine.initial_regval(params, w0)    # :231-233
+            have_current = False
+            converged = False
+            i = 1
+        else:
+            weights = engine.weights(state["weights"])
+            regVal, history = state["regVal"], state["history"]
+            have_current, converged, i = state["have_current"], state["converged"], state["i"]
+            log.warning("resuming at iteration %d from checkpoint %s", i, checkpoint)
+        last_saved = i
         while not converged and i <= numIterations:       # :237
             params.iteration = i
             folded, counts = engine.epoch(params, weights, with_counts=return_chain_counts)
@@ -394,10 +410,71 @@ class ParallelizedSGD:
             else:                                          # :295-297
                 log.warning("Iteration (%d/%d). The size of sampled batch is zero", i, numIterations)
             i += 1
+            if ckpt and (i - last_saved >= ckpt.every or converged or i > numIterations):
+                ckpt.save(fp, engine.to_host(weights), i, regVal, history, have_current, converged)
+                last_saved = i
         log.info("GradientDescent.runMiniBatchSGD finished. Last 10 stochastic losses %s",
                  ", ".join(str(v) for v in history[-10:]))
         out = (engine.to_host(weights), np.array(history))
         return out + (chain_counts,) if return_chain_counts else out
+
+
+_CKPT_VERSION = 1
+
+
+def _ckpt_fingerprint(params, data: PartitionedData, w0: np.ndarray) -> np.ndarray:
+    """What an iteration's result depends on besides (w, i): the plugins and hyper-parameters
+    (the psgd_params fields), the data's shape, the initial weights (the first regVal and the
+    driver's first convergence reference). numIterations is left out, so a finished run can be
+    resumed with a larger iteration budget and continue exactly where it stopped."""
+    import hashlib
+    h = hashlib.sha256()
+    for f, _ in N.psgd_params._fields_:
+        if f != "iteration":
+            h.update(f"{f}={getattr(params, f)!r};".encode())
+    h.update(f"n={data.count()};P={data.num_partitions};d={data.num_features};".encode())
+    h.update(np.ascontiguousarray(w0, dtype=np.float64).tobytes())
+    return np.frombuffer(h.digest(), dtype=np.uint8)
+
+
+class DriverCheckpoint:
+    """Checkpoint / resume of the driver loop (the reference has none and returns the
+    weights only, ParallelizedSGD.scala:304). The loop's whole state between iterations is
+    (weights, i, regVal, stochasticLossHistory, whether `currentWeights` is defined, converged):
+    an epoch is a pure function of (weights, i, data) -- the sample seed is 42 + i (:240), every
+    chain starts its updater status afresh (:246) -- so a resumed run continues bit for bit.
+
+    Written by rank 0 only (every rank holds the same folded state), atomically (temp file +
+    os.replace), as an .npz read back with allow_pickle=False."""
+
+    def __init__(self, path: str, every: int = 1):
+        _require(every >= 1, f"checkpoint interval must be positive but got {every}")
+        self.path, self.every = str(path), int(every)
+
+    def load(self, fingerprint: np.ndarray):
+        import os
+        if not os.path.exists(self.path):
+            return None
+        with np.load(self.path, allow_pickle=False) as z:
+            if int(z["version"]) != _CKPT_VERSION or not np.array_equal(z["fingerprint"], fingerprint):
+                raise IllegalArgumentException(
+                    f"checkpoint {self.path} was written by a run with other parameters or data")
+            return dict(weights=z["weights"].copy(), i=int(z["i"]), regVal=float(z["regVal"]),
+                        history=[float(v) for v in z["history"]],
+                        have_current=bool(z["have_current"]), converged=bool(z["converged"]))
+
+    def save(self, fingerprint, weights_host, i, regVal, history, have_current, converged):
+        import os
+        rank, _, _ = _dist()
+        if rank != 0:
+            return
+        tmp = f"{self.path}.tmp{os.getpid()}"
+        with open(tmp, "wb") as f:
+            np.savez(f, version=np.int64(_CKPT_VERSION), fingerprint=fingerprint,
+                     weights=np.asarray(weights_host, dtype=np.float64), i=np.int64(i),
+                     regVal=np.float64(regVal), history=np.asarray(history, dtype=np.float64),
+                     have_current=np.bool_(have_current), converged=np.bool_(converged))
+        os.replace(tmp, self.path)
 
 
 def max_j(a: float, b: float) -> float:
