@@ -58,7 +58,7 @@ def pmc_traffic(workload, grad, variant, storage, rows, compute="f32", updater="
     import glob
     files = glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_pmc.json")) + \
         glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_*_pmc.json"))
-    if not files or not (100 <= variant < 200 or 300 <= variant < 800):
+    if not files or not (100 <= variant < 200 or 300 <= variant < 900):
         return None, None
     waves = 0
     g = {"logistic": 0, "least_squares": 1, "hinge": 2}[grad]
@@ -69,6 +69,9 @@ def pmc_traffic(workload, grad, variant, storage, rows, compute="f32", updater="
     if variant < 200:   # chain_dense<S, T, GRAD, UPD, CONV = false, NV, FULL>
         cname = "float" if compute == "f32" else "double"
         prefix = f"psgd::chain_dense<{sname}, {cname}, {g}, {u}, false, {variant - 100},"
+    elif variant >= 800:   # chain_split<S, T, GRAD, UPD, NV, FULL, H>
+        cname = "float" if compute == "f32" else "double"
+        prefix = f"psgd::chain_split<{sname}, {cname}, {g}, {u}, {variant % 10},"
     elif variant >= 700:
         prefix = f"psgd::chain_block64<{sname}, {g}, {u}, {variant % 10}, "
         waves = 1 + (variant - 700) // 10
@@ -98,6 +101,10 @@ def pmc_traffic(workload, grad, variant, storage, rows, compute="f32", updater="
 
 
 def kernel_name(variant):
+    if 800 <= variant < 900:
+        h = (variant - 800) // 10
+        return (f"chain_split (NV={variant % 10}: per-sample chain, features split over {h} compute waves, "
+                f"partial dots exchanged through LDS)")
     if 700 <= variant < 800:
         waves = 1 + (variant - 700) // 10
         return (f"chain_block64 (NV={variant % 10}: blocked fp64 chain, 8-row Gram blocks, "

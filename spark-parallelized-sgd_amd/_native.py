@@ -11,7 +11,8 @@ import subprocess
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpsgd.so")
+# PSGD_LIB: another build of the same library (diagnostics, e.g. `make -C csrc stamps`)
+LIB_PATH = os.environ.get("PSGD_LIB") or os.path.join(HERE, "libpsgd.so")
 CSRC = os.path.join(HERE, "csrc")
 
 PSGD_OK, PSGD_EINVAL, PSGD_EUNSUPPORTED, PSGD_EDEVICE, PSGD_ENOMEM, PSGD_ESTATE = 0, -1, -2, -3, -4, -5

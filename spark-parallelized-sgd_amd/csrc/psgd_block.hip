@@ -580,6 +580,12 @@ __global__ __launch_bounds__(1024) void margin_loss_kernel(ChainLaunch L) {
     }
 }
 
+int launch_margin_loss(const ChainLaunch& L, int n_chains, hipStream_t st) {
+    if (!L.zbuf) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(margin_loss_kernel, dim3(n_chains), dim3(1024), 0, st, L);
+    return (int)hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------------------
 // Launcher.
 // ------------------------------------------------------------------------------------------

@@ -108,44 +108,9 @@ __host__ __device__ constexpr int row_lane64(int i) {
     return 32 * (i & 1) + 16 * ((i >> 1) & 1) + 8 * ((i >> 2) & 1);
 }
 
-// 1 / (1 + exp(m)) in f64 with a short dependent chain: the recurrence evaluates it once per row
-// on its critical path, where the library exp (Horner) and IEEE division (div_scale / div_fmas /
-// div_fixup) are ~30 dependent f64 operations. Here: exp(m) = 2^k e^r, k = rint(m log2 e),
-// r = m - k ln2 (two-part ln2, |r| <= ln2/2), e^r by its Taylor polynomial of degree 13
-// (truncation < 2e-16 relative) evaluated Estrin-style (depth 5 instead of 13), 2^k by ldexp;
-// the reciprocal by v_rcp_f64 and two Newton steps. Within ~2 ulp of the reference's
-// 1.0 / (1.0 + exp(margin)) (the fp64 mode's bar is 1e-9 relative). m is clamped to
-// [-746, 709] (exp(-746) is 0 in f64; beyond 709 the result is ~1e-308 instead of 0); a NaN
-// stays NaN.
 #ifndef PSGD_B64_FAST_SIGMOID
 #define PSGD_B64_FAST_SIGMOID 1
 #endif
-__device__ __forceinline__ double recip_one_plus_exp(double m) {
-    m = m > 709.0 ? 709.0 : m;
-    m = m < -746.0 ? -746.0 : m;
-    const double kd = __builtin_rint(m * 1.4426950408889634);
-    double r = __builtin_fma(-kd, 6.93147180369123816490e-01, m);   // ln2 high part
-    r = __builtin_fma(-kd, 1.90821492927058770002e-10, r);          // ln2 low part
-    const double r2 = r * r, r4 = r2 * r2, r8 = r4 * r4;
-    const double p01 = __builtin_fma(r, 1.0, 1.0);
-    const double p23 = __builtin_fma(r, 1.0 / 6, 0.5);
-    const double p45 = __builtin_fma(r, 1.0 / 120, 1.0 / 24);
-    const double p67 = __builtin_fma(r, 1.0 / 5040, 1.0 / 720);
-    const double p89 = __builtin_fma(r, 1.0 / 362880, 1.0 / 40320);
-    const double pab = __builtin_fma(r, 1.0 / 39916800, 1.0 / 3628800);
-    const double pcd = __builtin_fma(r, 1.0 / 6227020800.0, 1.0 / 479001600);
-    const double q03 = __builtin_fma(r2, p23, p01);
-    const double q47 = __builtin_fma(r2, p67, p45);
-    const double q8b = __builtin_fma(r2, pab, p89);
-    const double q07 = __builtin_fma(r4, q47, q03);
-    const double q8d = __builtin_fma(r4, pcd, q8b);
-    const double er = __builtin_fma(r8, q8d, q07);
-    const double d = 1.0 + __builtin_amdgcn_ldexp(er, (int)kd);
-    double y = __builtin_amdgcn_rcp(d);
-    y = __builtin_fma(y, __builtin_fma(-d, y, 1.0), y);
-    y = __builtin_fma(y, __builtin_fma(-d, y, 1.0), y);
-    return y;
-}
 
 // c = (-s) * mult(z, y): the step the row's gradient takes ([ext] MLlib 1.6.1 Gradient.compute,
 // SGDUpdater.scala:95 / :178 axpy(-thisIterStepSize, gradient, w)).

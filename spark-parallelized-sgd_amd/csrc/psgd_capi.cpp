@@ -958,7 +958,7 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         const char* e = getenv("PSGD_STAMPS");
         return e && *e && *e != '0';
     }();
-    if (want_stamps && layout == psgd::kCsr) {
+    if (want_stamps) {   // read by the CSR kernels and chain_split (and by PSGD_STAMPS builds)
         HIP_TRY(ctx->stamps.ensure((size_t)P * 16 * sizeof(unsigned long long)));
         HIP_TRY(hipMemsetAsync(ctx->stamps.p, 0, (size_t)P * 16 * sizeof(unsigned long long), st));
         L.stamps = ctx->stamps.as<unsigned long long>();
@@ -1042,7 +1042,10 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         if (L.stamps) {   // PSGD_STAMPS=1: per-chain cycle counters of the CSR fp32 kernels (stderr)
             // chain_sparse_lds: {chain, loader, tagger} x {total, waiting}; chain_sparse_spec:
             // {chain, helper} x {total, waiting}
-            const int KS = ctx->last_variant >= 600 ? 6 : 4;
+            // chain_split: {total, row + dot + reduce, exchange wait, multiplier + update} per
+            // compute wave
+            const bool split = ctx->last_variant >= 800;
+            const int KS = split ? 16 : ctx->last_variant >= 600 ? 6 : 4;
             std::vector<unsigned long long> h((size_t)P * 16);
             HIP_TRY(hipMemcpyAsync(h.data(), L.stamps, h.size() * 8, hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
@@ -1052,10 +1055,13 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
                     v[k].push_back((double)h[(size_t)p * KS + k] / std::max<int64_t>(n_max, 1));
             const char* n4[4] = {"chain.total", "chain.wait", "helper.total", "helper.wait"};
             const char* n6[6] = {"chain.total", "chain.wait", "loader.total", "loader.wait", "tagger.total", "tagger.wait"};
+            const char* ns[4] = {"total", "dot", "xwait", "update"};
             for (int k = 0; k < KS; ++k) {
                 std::sort(v[k].begin(), v[k].end());
-                fprintf(stderr, "psgd stamps %-18s cycles/row median %8.1f\n", KS == 6 ? n6[k] : n4[k],
-                        v[k][v[k].size() / 2]);
+                char nm[32];
+                if (split) snprintf(nm, sizeof nm, "wave%d.%s", k / 4, ns[k % 4]);
+                fprintf(stderr, "psgd stamps %-18s cycles/row median %8.1f\n",
+                        split ? nm : KS == 6 ? n6[k] : n4[k], v[k][v[k].size() / 2]);
             }
         }
         if (e == -2) return fail(PSGD_EUNSUPPORTED, "this gradient/updater/layout combination is not built");

@@ -153,6 +153,65 @@ __device__ __forceinline__ float pow_fast(float a, float b) {
 }
 __device__ __forceinline__ float m_fma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 
+// 1/sqrt(x) for x >= 1 in f64: v_rsq_f64 and two Newton steps (x = inf gives 0, NaN stays NaN).
+__device__ __forceinline__ double rsqrt_newton(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const double e = __builtin_fma(-(x * y), y, 1.0);
+        y = __builtin_fma(0.5 * y, e, y);
+    }
+    return x == __builtin_inf() ? 0.0 : y;
+}
+
+// pow(r, iter) of AdamSGDUpdater's fix1 (UPD.scala:262) for iter = j >= 1: when iter * log2(r) <
+// -1100 the power is below 2^-1100 and the library pow returns 0 (it rounds below half the
+// least denormal); the hardware f32 log2 (relative error ~1e-7, so the margin to 2^-1075 is
+// ~25 binades) decides that without the ~100-instruction f64 pow, which after a few hundred
+// samples no coordinate needs (r is an average of squared gradients, well below 1).
+__device__ __forceinline__ double pow_int_iter(double r, double iter) {
+    const float l2 = __builtin_amdgcn_logf((float)r);
+    double p = 0.0;
+    if (!((float)iter * l2 < -1100.0f)) p = pow(r, iter);
+    return p;
+}
+
+// 1 / (1 + exp(m)) in f64 with a short dependent chain: the chains evaluate it once per row on
+// their critical path, where the library exp (Horner) and IEEE division (div_scale / div_fmas /
+// div_fixup) are ~30 dependent f64 operations. Here: exp(m) = 2^k e^r, k = rint(m log2 e),
+// r = m - k ln2 (two-part ln2, |r| <= ln2/2), e^r by its Taylor polynomial of degree 13
+// (truncation < 2e-16 relative) evaluated Estrin-style (depth 5 instead of 13), 2^k by ldexp;
+// the reciprocal by v_rcp_f64 and two Newton steps. Within ~2 ulp of the reference's
+// 1.0 / (1.0 + exp(margin)) (the fp64 mode's bar is 1e-9 relative). m is clamped to
+// [-746, 709] (exp(-746) is 0 in f64; beyond 709 the result is ~1e-308 instead of 0); a NaN
+// stays NaN.
+__device__ __forceinline__ double recip_one_plus_exp(double m) {
+    m = m > 709.0 ? 709.0 : m;
+    m = m < -746.0 ? -746.0 : m;
+    const double kd = __builtin_rint(m * 1.4426950408889634);
+    double r = __builtin_fma(-kd, 6.93147180369123816490e-01, m);   // ln2 high part
+    r = __builtin_fma(-kd, 1.90821492927058770002e-10, r);          // ln2 low part
+    const double r2 = r * r, r4 = r2 * r2, r8 = r4 * r4;
+    const double p01 = __builtin_fma(r, 1.0, 1.0);
+    const double p23 = __builtin_fma(r, 1.0 / 6, 0.5);
+    const double p45 = __builtin_fma(r, 1.0 / 120, 1.0 / 24);
+    const double p67 = __builtin_fma(r, 1.0 / 5040, 1.0 / 720);
+    const double p89 = __builtin_fma(r, 1.0 / 362880, 1.0 / 40320);
+    const double pab = __builtin_fma(r, 1.0 / 39916800, 1.0 / 3628800);
+    const double pcd = __builtin_fma(r, 1.0 / 6227020800.0, 1.0 / 479001600);
+    const double q03 = __builtin_fma(r2, p23, p01);
+    const double q47 = __builtin_fma(r2, p67, p45);
+    const double q8b = __builtin_fma(r2, pab, p89);
+    const double q07 = __builtin_fma(r4, q47, q03);
+    const double q8d = __builtin_fma(r4, pcd, q8b);
+    const double er = __builtin_fma(r8, q8d, q07);
+    const double d = 1.0 + __builtin_amdgcn_ldexp(er, (int)kd);
+    double y = __builtin_amdgcn_rcp(d);
+    y = __builtin_fma(y, __builtin_fma(-d, y, 1.0), y);
+    y = __builtin_fma(y, __builtin_fma(-d, y, 1.0), y);
+    return y;
+}
+
 // java.lang.Math.max(a, b): NaN if either is NaN.
 template <typename T>
 __device__ __forceinline__ T jmax(T a, T b) {

@@ -76,7 +76,7 @@ struct ChainLaunch {
 // Kernel variants (*kernel_variant, psgd_ctx_last_kernel): 100 + NV chain_dense, 200 + LAYOUT
 // chain_general, 300 + NV chain_block, 400 + storage chain_sparse, 410 + storage chain_sparse_spec,
 // 500 + LAYOUT chain_multinomial, 600 + 10 (SK 8) + 20 (fp64) + storage chain_sparse_lds,
-// 700 + 10 (H - 1) + NV chain_block64.
+// 700 + 10 (H - 1) + NV chain_block64, 800 + 10 H + NV chain_split.
 // *weights_in_wf32 (nullable): the launch left each chain's weights in L.wf32 (w = walpha v, the
 // fp32 CSR kernels), to be folded by launch_fold_f32; else they are in L.w_out.
 int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int storage, int compute,
@@ -99,6 +99,8 @@ int launch_block64_chains(const ChainLaunch& L, const KParams& kp, int storage, 
                           hipStream_t stream, int* kernel_variant);
 // lossSum of fp64 Logistic chains from the per-row dots in L.zbuf64 (psgd_kernels.hip).
 int launch_logistic_loss64(const ChainLaunch& L, int n_chains, hipStream_t stream);
+// lossSum of fp32 Logistic chains from the per-row margins in L.zbuf (psgd_block.hip).
+int launch_margin_loss(const ChainLaunch& L, int n_chains, hipStream_t stream);
 int launch_fold(const double* w, int64_t w_stride, const double* rv, const double* loss,
                 const double* cnt, int64_t s_stride, int n, int d, double* out,
                 const int* watchdog, hipStream_t stream);

@@ -20,33 +20,11 @@
 // norms are reassociated (wave tree instead of the F2J left fold), so fp64 mode agrees with the
 // reference to rounding, not bitwise.
 #include "psgd_device.h"
+#include "psgd_split.h"
 
 #include <stdlib.h>
 
 namespace psgd {
-
-// 1/sqrt(x) for x >= 1 in f64: v_rsq_f64 and two Newton steps (x = inf gives 0, NaN stays NaN).
-__device__ __forceinline__ double rsqrt_newton(double x) {
-    double y = __builtin_amdgcn_rsq(x);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const double e = __builtin_fma(-(x * y), y, 1.0);
-        y = __builtin_fma(0.5 * y, e, y);
-    }
-    return x == __builtin_inf() ? 0.0 : y;
-}
-
-// pow(r, iter) of AdamSGDUpdater's fix1 (UPD.scala:262) for iter = j >= 1: when iter * log2(r) <
-// -1100 the power is below 2^-1100 and the library pow returns 0 (it rounds below half the
-// least denormal); the hardware f32 log2 (relative error ~1e-7, so the margin to 2^-1075 is
-// ~25 binades) decides that without the ~100-instruction f64 pow, which after a few hundred
-// samples no coordinate needs (r is an average of squared gradients, well below 1).
-__device__ __forceinline__ double pow_int_iter(double r, double iter) {
-    const float l2 = __builtin_amdgcn_logf((float)r);
-    double p = 0.0;
-    if (!((float)iter * l2 < -1100.0f)) p = pow(r, iter);
-    return p;
-}
 
 template <typename S, typename T, int GRAD, int UPD, bool CONV, int NV, bool FULL>
 __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, RingGeom geom) {
@@ -941,6 +919,11 @@ int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int stora
     if (!per_sample && layout == kCsr && compute == 0 &&
         sparse_lds64_applies(kp.d, max_nnz, updater, check_conv, kp.alpha_ok != 0) && L.wf32)
         return launch_sparse_lds64_chains(L, kp, storage, gradient, updater, max_nnz, stream, kernel_variant);
+    if (!per_sample && split_path_applies(layout, updater, check_conv, storage, max_ld)) {
+        const int e = launch_split_chains(L, kp, storage, compute, gradient, updater, min_ld, max_ld,
+                                          lds_spread, stream, kernel_variant);
+        if (e != -3) return e;
+    }
     const size_t lds = (size_t)(lds_spread > 0 ? lds_spread : 0);
     if (storage == 1)
         return dispatch_grad<float>(L, kp, layout, compute, gradient, updater, check_conv, min_ld,

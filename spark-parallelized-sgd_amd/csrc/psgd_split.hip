@@ -1,0 +1,533 @@
+// psgd_split.hip -- the per-sample dense chain with the feature dimension split over H compute
+// waves (gfx950): the throughput kernel of the stateful updaters.
+//
+// Reference (paths under /root/reference, src/main/scala/org/apache/spark/mllib/optimization/):
+//   chain loop      ParallelizedSGD.scala:243-270 (one chain per partition, per-sample updates)
+//   AdaGrad         SGDUpdater.scala:193-227  (status r += g*g; w += -s/sqrt(j) * g / (r + 1)^0.5)
+//   Adam            SGDUpdater.scala:238-286  (v, r; fix1 = (1 - r^iter)^0.5 + eps; lr = s / (1 - beta^iter))
+//   gradients       [ext] MLlib 1.6.1 Gradient.scala (mult * x), as in psgd_kernels.hip
+//
+// AdaGrad / Adam keep per-feature status that depends non-linearly on each sample's gradient, so
+// the blocked Gram form of chain_block / chain_block64 does not apply: the chain is sequential
+// per sample. chain_dense runs it on one wave, whose per-sample path (a d-long dot, the wave
+// reduction, the multiplier, d status + weight updates with a reciprocal square root or a power
+// each) is ~2,000 cycles at d = 1,024 in fp32. Here the features are split over H compute waves,
+// one per SIMD: wave h owns the row vectors [h NV/H, (h+1) NV/H) of W, of the status and of every
+// row. Per sample each wave takes its partial dot, reduces it across its lanes and publishes it
+// in LDS as tagged 64-bit words ({32 bits of the partial, sample number + 1}: one word per fp32
+// partial, two per fp64 one), so a reader needs no separate flag: it polls the H words of the
+// sample's parity slot until every tag is the sample's. All waves add the partials in wave order
+// (((p0 + p1) + p2) + p3) -- bit-identical -- run the identical scalar multiplier, and update
+// only their own features. A parity slot is rewritten two samples later, only after every wave
+// has published the sample in between (which it does after reading this one).
+//
+// Rows stream through the LDS ring of chain_dense (ring_loader, one loader wave); compute wave 0
+// hands slots back: when it has every partial of sample t, all waves have read row t + 1.
+// The per-element arithmetic is chain_dense's, operator for operator (this file is compiled with
+// -ffp-contract=off); only the dot is reassociated (per-wave partials, wave trees, the fixed
+// order above), inside the fp64 mode's 1e-9 relative bar. Logistic's multiplier is on every
+// sample's critical path: fp64 takes chain_block64's short-chain 1/(1 + exp(m)) (within ~2 ulp),
+// fp32 the hardware exp2 / reciprocal (as chain_block); the row losses (log1pExp) are summed
+// after the chain from the stored margins, off the sequential path.
+#include "psgd_device.h"
+#include "psgd_split.h"
+
+#include <stdlib.h>
+
+#include <type_traits>
+
+// compute waves per chain: min(NV, PSGD_SPLIT_HMAX), one per SIMD
+#ifndef PSGD_SPLIT_HMAX
+#define PSGD_SPLIT_HMAX 4
+#endif
+
+namespace psgd {
+
+namespace {
+
+// The SIMD a wave runs on (HW_REG_HW_ID bits 5:4).
+__device__ __forceinline__ unsigned split_simd() {
+    unsigned id;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(id));
+    return (id >> 4) & 3;
+}
+
+// Roles of the H + 1 waves from their SIMDs (the same answer in every wave): compute waves 0 ..
+// H-1 on distinct SIMDs where the dispatcher allows it, the remaining wave is the loader (H).
+template <int H>
+__device__ __forceinline__ int split_role(const unsigned* simd, int w) {
+    constexpr int NW = H + 1;
+    int role[NW];
+    bool used[4] = {false, false, false, false};
+    int nc = 0;
+    for (int i = 0; i < NW; ++i) role[i] = -1;
+    for (int i = 0; i < NW; ++i)
+        if (!used[simd[i] & 3] && nc < H) { used[simd[i] & 3] = true; role[i] = nc++; }
+    for (int i = 0; i < NW; ++i)
+        if (role[i] < 0 && nc < H) role[i] = nc++;
+    for (int i = 0; i < NW; ++i)
+        if (role[i] < 0) role[i] = H;
+    return role[w];
+}
+
+__device__ __forceinline__ void lds_write_u64(uint64_t* p, uint64_t v) {
+    asm volatile("ds_write_b64 %0, %1" : : "v"((unsigned)(uintptr_t)p), "v"(v) : "memory");
+}
+__device__ __forceinline__ uint64_t lds_read_u64(const uint64_t* p) {
+    uint64_t v;
+    asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"((unsigned)(uintptr_t)p) : "memory");
+    return v;
+}
+
+// fixed LDS area: [RingHeader 16 B][exchange 2 x H x PC u64][SIMD ids of the H + 1 waves]
+template <int H, int PC>
+constexpr size_t split_fixed_bytes() {
+    return (sizeof(RingHeader) + 2 * H * PC * 8 + (H + 1) * 4 + 15) / 16 * 16;
+}
+
+}  // namespace
+
+template <typename S, typename T, int GRAD, int UPD, int NV, bool FULL, int H>
+__global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KParams kp, RingGeom geom) {
+    using V = typename Vec16<S>::type;
+    constexpr int VEC = Vec16<S>::N;
+    constexpr int NVH = NV / H;              // row vectors of one compute wave
+    constexpr int E = NVH * VEC;             // features per lane of one compute wave
+    constexpr int E2 = E / 2;
+    constexpr int ROW_BYTES = NV * 1024;
+    constexpr int PC = sizeof(T) / 4;        // 32-bit pieces of a partial
+    constexpr int XW = H * PC;               // exchange words per sample
+    static_assert(NV % H == 0 && E % 2 == 0, "the compute waves split the row vectors evenly");
+    static_assert(XW <= 64, "one lane per exchange word");
+    // Logistic: the per-row dots go to L.zbuf64 / L.zbuf, the losses are summed after the chain
+    constexpr bool ZOUT = GRAD == G_LOGISTIC;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    RingHeader* hdr = reinterpret_cast<RingHeader*>(smem);
+    uint64_t* xw = reinterpret_cast<uint64_t*>(smem + sizeof(RingHeader));
+    unsigned* simd_of = reinterpret_cast<unsigned*>(xw + 2 * XW);
+    char* meta_ring = smem + split_fixed_bytes<H, PC>();
+    char* ring = meta_ring + geom.meta_blocks * kMetaBlockBytes;
+
+    const int lane = threadIdx.x & 63;
+    const int chain = blockIdx.x;
+    const ChainDesc dsc = L.descs[chain];
+    const int d = kp.d;
+    const int64_t n = dsc.n_rows;
+    const int MB = geom.meta_blocks;
+
+    if (threadIdx.x == 0) {
+        hdr->ready = 0;
+        hdr->consumed = 0;
+        hdr->stop = 0;
+        hdr->consumed1 = 0;
+    }
+    for (int i = threadIdx.x; i < 2 * XW; i += blockDim.x) xw[i] = 0;   // tag 0: no sample yet
+    // every wave's SIMD, for the roles
+    if (lane == 0) simd_of[threadIdx.x >> 6] = split_simd();
+    __syncthreads();
+    const int h = __builtin_amdgcn_readfirstlane(split_role<H>(simd_of, threadIdx.x >> 6));
+    __syncthreads();
+
+    if (h == H) {
+        ring_loader<S, NV, FULL, 4>(L, dsc, hdr, meta_ring, ring, geom, lane);
+        return;
+    }
+
+    // ---------------- compute wave h ----------------
+    using T2 = T __attribute__((ext_vector_type(2)));
+    T2 w[E2];
+#pragma unroll
+    for (int u = 0; u < NVH; ++u) {
+        const int base = ((h * NVH + u) * 64 + lane) * VEC;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            const int f = base + k;
+            const double wv = as_global(L.w_in)[f < d ? f : 0];   // unconditional, clamped
+            w[(u * VEC + k) / 2][(u * VEC + k) % 2] = f < d ? T(wv) : T(0);
+        }
+    }
+    // status (UPD.scala:193-286) in registers beside the weights: ua = AdaGrad's accumulator or
+    // Adam's v, ub = Adam's r; the chain's first sample takes the reference's `None` branch
+    constexpr bool STATE_B = UPD == U_ADAM;
+    T2 ua[E2], ub[STATE_B ? E2 : 1];
+#pragma unroll
+    for (int e = 0; e < E2; ++e) ua[e] = T2{T(0), T(0)};
+#pragma unroll
+    for (int e = 0; e < (STATE_B ? E2 : 1); ++e) ub[e] = T2{T(0), T(0)};
+
+    // this wave's slice of rows t and t+1 (ping-pong), read from the ring
+    T2 xb[2][E2];
+    double yb[2], sb[2];
+    int meta_blk = 0;
+    // the LDS reads of row t's slice and meta into buffer p (issued here, waited for at first use)
+    auto read_row = [&](auto pc, const char* src, int64_t t) __attribute__((always_inline)) {
+        constexpr int p = decltype(pc)::value;
+#pragma unroll
+        for (int u = 0; u < NVH; ++u) {
+            const int v = h * NVH + u;
+            V xv = *reinterpret_cast<const V*>(src + v * 1024 + lane * 16);
+            if constexpr (!FULL) {
+                // vectors past the row end were not loaded: their LDS bytes are stale
+                if ((v * 64 + lane) * VEC >= dsc.ld) xv = V(0);
+            }
+            T tmp[VEC];
+            unpack<S, T>(xv, tmp);
+#pragma unroll
+            for (int k = 0; k < VEC; k += 2) xb[p][(u * VEC + k) / 2] = T2{tmp[k], tmp[k + 1]};
+        }
+        if (t > 0 && (t & (kMetaRows - 1)) == 0) meta_blk = (meta_blk + 1 == MB) ? 0 : meta_blk + 1;
+        const f64x2 meta = *reinterpret_cast<const f64x2*>(
+            meta_ring + meta_blk * kMetaBlockBytes + (int)(t & (kMetaRows - 1)) * 16);
+        yb[p] = meta.x;
+        sb[p] = meta.y;
+    };
+
+    // Spin until `rows` rows have landed (rare: the loader runs a ring ahead). Only `ready`
+    // leaves the branch, so no LDS read waits at its join. false: the chain stopped.
+    unsigned ready = 0;
+    bool stop = false;
+    auto wait_rows = [&](int64_t rows) __attribute__((always_inline)) {
+        if (rows > (int64_t)ready) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            for (;;) {
+                ready = __hip_atomic_load(&hdr->ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (rows <= (int64_t)ready) break;
+                if (__hip_atomic_load(&hdr->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) { stop = true; break; }
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kWatchdogTicks) {
+                    __hip_atomic_fetch_or(L.watchdog, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    stop = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+    };
+
+    // The exchange of sample t: publish writes this wave's partial (lanes 0 .. PC-1, one word
+    // each); collect polls the XW words of the parity slot (lane l reads word l) until all carry
+    // the sample's tag and returns their sum in wave order. A stopped chain leaves collect with
+    // whatever it read (the host raises on the watchdog word).
+    constexpr uint64_t kMask = XW == 64 ? ~0ull : ((1ull << XW) - 1);
+    auto publish = [&](T zh, int64_t t) __attribute__((always_inline)) {
+        uint32_t piece;
+        if constexpr (PC == 1) {
+            piece = __float_as_uint(zh);
+        } else {
+            const uint64_t b = (uint64_t)__double_as_longlong(zh);
+            piece = lane == 0 ? (uint32_t)b : (uint32_t)(b >> 32);
+        }
+        if (lane < PC)
+            lds_write_u64(xw + (int)(t & 1) * XW + h * PC + lane, ((uint64_t)(uint32_t)(t + 1) << 32) | piece);
+    };
+    auto collect = [&](int64_t t) __attribute__((always_inline)) -> T {
+        const uint32_t tag = (uint32_t)(t + 1);
+        const uint64_t* src = xw + (int)(t & 1) * XW + (lane < XW ? lane : 0);
+        uint64_t v = lds_read_u64(src);
+        if ((__ballot((uint32_t)(v >> 32) == tag) & kMask) != kMask) {
+            // spin on the LDS words alone (s_memrealtime is a scalar-memory round trip that the
+            // next LDS wait would also wait for); the stop flag and the clock every 1024 polls
+            uint64_t t0 = 0;
+            for (unsigned spin = 1;; ++spin) {
+                v = lds_read_u64(src);
+                if ((__ballot((uint32_t)(v >> 32) == tag) & kMask) == kMask) break;
+                if ((spin & 1023) == 0) {
+                    if (__hip_atomic_load(&hdr->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) { stop = true; break; }
+                    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+                    if (t0 == 0) t0 = now;
+                    if (now - t0 > kWatchdogTicks) {
+                        __hip_atomic_fetch_or(L.watchdog, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        stop = true;
+                        break;
+                    }
+                }
+            }
+        }
+        const int lo = (int)(uint32_t)v;
+        T acc = T(0);
+#pragma unroll
+        for (int g = 0; g < H; ++g) {
+            T pg;
+            if constexpr (PC == 1) {
+                pg = __int_as_float(__builtin_amdgcn_readlane(lo, g));
+            } else {
+                const uint32_t a = (uint32_t)__builtin_amdgcn_readlane(lo, 2 * g);
+                const uint32_t b = (uint32_t)__builtin_amdgcn_readlane(lo, 2 * g + 1);
+                pg = __longlong_as_double((long long)(((uint64_t)b << 32) | a));
+            }
+            acc = g == 0 ? pg : acc + pg;
+        }
+        return acc;
+    };
+
+    double loss_sum = 0.0;
+    T loss_blk = T(0);          // fp32 mode: block partial, flushed to the fp64 sum every 32 rows
+    T* zout = nullptr;
+    if constexpr (ZOUT) {
+        if constexpr (sizeof(T) == 8) zout = L.zbuf64 + (int64_t)chain * L.zstride;
+        else zout = L.zbuf + (int64_t)chain * L.zstride;
+    }
+    const char* slot_ptr = ring;
+    const char* const ring_end = ring + geom.rows * ROW_BYTES;
+
+    // diagnostic builds (-DPSGD_STAMPS): cycles per phase of this wave's samples
+    PSGD_STAMP(uint64_t st_dot = 0, st_x = 0, st_upd = 0; const uint64_t st_begin = __builtin_amdgcn_s_memtime();
+               uint64_t st_mark = st_begin;)
+#define SPLIT_STAMP(acc) PSGD_STAMP({ const uint64_t now_ = __builtin_amdgcn_s_memtime(); acc += now_ - st_mark; st_mark = now_; })
+
+    // Sample t (row t in xb[p]): the partial dot and its wave reduction, publish; the reads of
+    // row t + 1 go out before the poll so that their LDS latency overlaps the exchange's; then
+    // the multiplier and this wave's updates. Straight-line: the only branches spin.
+    auto sample = [&](auto pc, int64_t t) __attribute__((always_inline)) {
+        constexpr int p = decltype(pc)::value;
+        const T y = T(yb[p]);
+        const T s = T(sb[p]);
+        const T2* x = xb[p];
+        T2 a0 = T2{T(0), T(0)}, a1 = T2{T(0), T(0)};
+#pragma unroll
+        for (int e = 0; e < E2; e += 2) {
+            a0 = __builtin_elementwise_fma(x[e], w[e], a0);
+            if (e + 1 < E2) a1 = __builtin_elementwise_fma(x[e + 1], w[e + 1], a1);
+        }
+        const T2 a = a0 + a1;
+        publish(wave_sum_uniform(a.x + a.y), t);
+        SPLIT_STAMP(st_dot);
+
+        const char* next_ptr = slot_ptr + ROW_BYTES;
+        if (next_ptr == ring_end) next_ptr = ring;
+        wait_rows(t + 2 < n ? t + 2 : n);
+        read_row(std::integral_constant<int, 1 - p>{}, next_ptr, t + 1);   // past the end: unused
+        slot_ptr = next_ptr;
+
+        const T z = collect(t);
+        SPLIT_STAMP(st_x);
+        if (h == 0 && ((t & 1) == 1 || t + 1 == n)) {
+            // every wave has published sample t, so every wave has read rows <= t + 1
+            __hip_atomic_store(&hdr->consumed, (unsigned)(t + 1), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+
+        T mult;
+        if constexpr (ZOUT) {
+            // 1/(1 + exp(margin)) - y, margin = -z; the row's loss from z after the chain
+            if constexpr (sizeof(T) == 8) mult = recip_one_plus_exp(-z) - y;
+            else mult = __builtin_amdgcn_rcpf(1.0f + __expf(-z)) - y;
+            if (h == 0 && lane == 0) zout[t] = z;
+        } else {
+            T loss;
+            if constexpr (GRAD == G_LEAST_SQUARES) {
+                mult = z - y;
+                loss = mult * mult;   // halved once at the end (chain_dense)
+            } else {
+                loss = gradient_scalar<GRAD, T>(z, y, mult);
+            }
+            if constexpr (sizeof(T) == 4) {
+                loss_blk += loss;
+                if ((t & 31) == 31) { loss_sum += double(loss_blk); loss_blk = T(0); }
+            } else {
+                loss_sum += loss;
+            }
+        }
+
+        const T a_s = -s;
+        const bool first = t == 0;
+        const T iter = T(t + 1);
+        T al = T(0);
+        if constexpr (UPD == U_ADAM) {
+            if constexpr (sizeof(T) == 4) al = -(s / (T(1) - pow_fast(T(kp.beta), iter)));
+            else al = -(s / (T(1) - m_pow(T(kp.beta), iter)));
+        }
+#pragma unroll
+        for (int e = 0; e < E2; ++e) {
+            const T2 old = w[e];
+            T2 nw;
+            if constexpr (UPD == U_ADAGRAD) {
+                // accum = None ? g*g : accum + g*g; w += -s * (g / sqrt(accum + 1.0))
+                const T2 g = mult * x[e];
+                const T2 acc2 = first ? g * g : ua[e] + g * g;
+                ua[e] = acc2;
+                if constexpr (sizeof(T) == 4) {
+                    nw.x = old.x + a_s * (g.x * __builtin_amdgcn_rsqf(acc2.x + T(1)));
+                    nw.y = old.y + a_s * (g.y * __builtin_amdgcn_rsqf(acc2.y + T(1)));
+                } else {
+                    nw.x = old.x + a_s * (g.x * rsqrt_newton(acc2.x + T(1)));
+                    nw.y = old.y + a_s * (g.y * rsqrt_newton(acc2.y + T(1)));
+                }
+            } else {
+                // Adam, the reference's variant: v = beta v + (1-beta) g, r = gamma r + (1-gamma) g^2,
+                // fix1 = sqrt(1 - r^iter) + eps, w += -lr * v / fix1
+                const T beta = T(kp.beta), gamma = T(kp.gamma);
+                const T2 g = mult * x[e];
+                const T2 sq = g * g;
+                T2 v, r;
+                if (first) { v = g * (T(1) - beta); r = sq * (T(1) - gamma); }
+                else { v = ua[e] * beta + g * (T(1) - beta); r = ub[e] * gamma + sq * (T(1) - gamma); }
+                ua[e] = v;
+                ub[e] = r;
+                if constexpr (sizeof(T) == 4) {
+                    const T fx = __builtin_amdgcn_sqrtf(T(1) - pow_fast(r.x, iter)) + T(kp.eps);
+                    const T fy = __builtin_amdgcn_sqrtf(T(1) - pow_fast(r.y, iter)) + T(kp.eps);
+                    nw.x = old.x + al * (v.x * __builtin_amdgcn_rcpf(fx));
+                    nw.y = old.y + al * (v.y * __builtin_amdgcn_rcpf(fy));
+                } else {
+                    const T fx = m_sqrt(T(1) - pow_int_iter(r.x, iter)) + T(kp.eps);
+                    const T fy = m_sqrt(T(1) - pow_int_iter(r.y, iter)) + T(kp.eps);
+                    nw.x = old.x + al * (v.x / fx);
+                    nw.y = old.y + al * (v.y / fy);
+                }
+            }
+            w[e] = nw;
+        }
+        SPLIT_STAMP(st_upd);
+    };
+
+    if (n > 0) {
+        wait_rows(1);
+        read_row(std::integral_constant<int, 0>{}, ring, 0);
+    }
+    int64_t t = 0;
+    for (; t + 2 <= n && !stop; t += 2) {
+        sample(std::integral_constant<int, 0>{}, t);
+        sample(std::integral_constant<int, 1>{}, t + 1);
+    }
+    if (t < n && !stop) sample(std::integral_constant<int, 0>{}, t++);
+    const int64_t count = t;   // n unless the chain stopped (then the host raises)
+    if constexpr (sizeof(T) == 4) loss_sum += double(loss_blk);
+    PSGD_STAMP(if (L.stamps && lane == 0) {
+        unsigned long long* o = L.stamps + (size_t)chain * 16 + 4 * h;
+        o[0] = st_mark - st_begin;
+        o[1] = st_dot;
+        o[2] = st_x;
+        o[3] = st_upd;
+    })
+#undef SPLIT_STAMP
+
+    // weights of this wave's features
+    double* wo = L.w_out + (int64_t)chain * d;
+#pragma unroll
+    for (int u = 0; u < NVH; ++u) {
+        const int base = ((h * NVH + u) * 64 + lane) * VEC;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k)
+            if (base + k < d) wo[base + k] = double(w[(u * VEC + k) / 2][(u * VEC + k) % 2]);
+    }
+    if (h > 0) return;
+    if constexpr (GRAD == G_LEAST_SQUARES) loss_sum = loss_sum / 2.0;
+    if (lane == 0) {
+        L.rv[chain] = 0.0;   // AdaGrad / Adam return regVal 0.0 (UPD.scala:221, :266)
+        if constexpr (!ZOUT) L.loss[chain] = loss_sum;
+        L.cnt[chain] = count;
+        L.cnt_d[chain] = double(count);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Launcher.
+// ------------------------------------------------------------------------------------------
+namespace {
+
+template <typename S>
+int split_nv(int64_t max_ld) {
+    constexpr int VEC = 16 / sizeof(S);
+    int nv = 1;
+    while (nv * 64 * VEC < max_ld) nv *= 2;
+    return nv;
+}
+
+template <typename S, typename T, int GRAD, int UPD, int NV>
+int launch_split(const ChainLaunch& L, const KParams& kp, bool full, size_t lds, hipStream_t st) {
+    constexpr int H = NV < PSGD_SPLIT_HMAX ? NV : PSGD_SPLIT_HMAX;
+    constexpr int PC = sizeof(T) / 4;
+    constexpr int ROW = NV * 1024;
+    constexpr size_t FIX = split_fixed_bytes<H, PC>();
+    const size_t budget = lds > 0 ? lds : (size_t)64 * 1024;
+    const int D = loader_depth<NV>();
+    int R = (int)((budget - FIX - 3 * kMetaBlockBytes) / ROW);
+    int MB = (R + kMetaRows - 1) / kMetaRows + 2;
+    while (R > 0 && FIX + (size_t)MB * kMetaBlockBytes + (size_t)R * ROW > budget) {
+        --R;
+        MB = (R + kMetaRows - 1) / kMetaRows + 2;
+    }
+    if (R < 6) return (int)hipErrorInvalidValue;   // the ring needs >= PUB + 2 slots
+    if constexpr (GRAD == G_LOGISTIC) {
+        // the rows' margins / dots, summed into the loss after the chain
+        if (sizeof(T) == 8 ? !L.zbuf64 : !L.zbuf) return (int)hipErrorInvalidValue;
+    }
+    RingGeom g{R, MB, D, 0};
+    const size_t bytes = FIX + (size_t)MB * kMetaBlockBytes + (size_t)R * ROW;
+    auto k = full ? chain_split<S, T, GRAD, UPD, NV, true, H> : chain_split<S, T, GRAD, UPD, NV, false, H>;
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(64 * (H + 1)), bytes, st, L, kp, g);
+    if constexpr (GRAD == G_LOGISTIC) {
+        const int e = (int)hipGetLastError();
+        if (e) return e;
+        if constexpr (sizeof(T) == 8) return launch_logistic_loss64(L, kp.n_chains, st);
+        else return launch_margin_loss(L, kp.n_chains, st);
+    }
+    return (int)hipGetLastError();
+}
+
+template <typename S, typename T, int GRAD, int UPD>
+int split_dispatch_nv(const ChainLaunch& L, const KParams& kp, int64_t min_ld, int64_t max_ld, size_t lds,
+                      hipStream_t st, int* variant) {
+    constexpr int VEC = 16 / sizeof(S);
+    const int nv = split_nv<S>(max_ld);
+    const bool full = min_ld >= (int64_t)nv * 64 * VEC;
+    if (variant) *variant = 800 + 10 * (nv < PSGD_SPLIT_HMAX ? nv : PSGD_SPLIT_HMAX) + nv;
+    switch (nv) {
+    case 2: return launch_split<S, T, GRAD, UPD, 2>(L, kp, full, lds, st);
+    case 4: return launch_split<S, T, GRAD, UPD, 4>(L, kp, full, lds, st);
+    case 8: return launch_split<S, T, GRAD, UPD, 8>(L, kp, full, lds, st);
+    default: return -3;
+    }
+}
+
+template <typename S, typename T, int GRAD>
+int split_dispatch_upd(const ChainLaunch& L, const KParams& kp, int updater, int64_t min_ld, int64_t max_ld,
+                       size_t lds, hipStream_t st, int* variant) {
+    if (updater == U_ADAGRAD) return split_dispatch_nv<S, T, GRAD, U_ADAGRAD>(L, kp, min_ld, max_ld, lds, st, variant);
+    if (updater == U_ADAM) return split_dispatch_nv<S, T, GRAD, U_ADAM>(L, kp, min_ld, max_ld, lds, st, variant);
+    return -3;
+}
+
+template <typename S, typename T>
+int split_dispatch_grad(const ChainLaunch& L, const KParams& kp, int gradient, int updater, int64_t min_ld,
+                        int64_t max_ld, size_t lds, hipStream_t st, int* variant) {
+    switch (gradient) {
+    case G_LOGISTIC: return split_dispatch_upd<S, T, G_LOGISTIC>(L, kp, updater, min_ld, max_ld, lds, st, variant);
+    case G_LEAST_SQUARES: return split_dispatch_upd<S, T, G_LEAST_SQUARES>(L, kp, updater, min_ld, max_ld, lds, st, variant);
+    case G_HINGE: return split_dispatch_upd<S, T, G_HINGE>(L, kp, updater, min_ld, max_ld, lds, st, variant);
+    default: return -3;
+    }
+}
+
+}  // namespace
+
+bool split_path_applies(int layout, int updater, bool check_conv, int storage, int64_t max_ld) {
+    if (layout != kDense || check_conv) return false;
+    if (updater != U_ADAGRAD && updater != U_ADAM) return false;
+    // PSGD_SPLIT=0 keeps chain_dense (A/B measurements)
+    static const bool off = [] {
+        const char* e = getenv("PSGD_SPLIT");
+        return e && *e == '0';
+    }();
+    if (off) return false;
+    const int nv = storage == 1 ? split_nv<float>(max_ld) : split_nv<double>(max_ld);
+    return nv >= 2 && nv <= 8;
+}
+
+int launch_split_chains(const ChainLaunch& L, const KParams& kp, int storage, int compute, int gradient,
+                        int updater, int64_t min_ld, int64_t max_ld, int lds_spread, hipStream_t st,
+                        int* variant) {
+    if (!split_path_applies(kDense, updater, false, storage, max_ld)) return -3;
+    const size_t lds = (size_t)(lds_spread > 0 ? lds_spread : 0);
+    if (storage == 1) {
+        if (compute == 1) return split_dispatch_grad<float, float>(L, kp, gradient, updater, min_ld, max_ld, lds, st, variant);
+        return split_dispatch_grad<float, double>(L, kp, gradient, updater, min_ld, max_ld, lds, st, variant);
+    }
+    if (compute == 1) return split_dispatch_grad<double, float>(L, kp, gradient, updater, min_ld, max_ld, lds, st, variant);
+    return split_dispatch_grad<double, double>(L, kp, gradient, updater, min_ld, max_ld, lds, st, variant);
+}
+
+}  // namespace psgd

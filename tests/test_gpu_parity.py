@@ -42,6 +42,15 @@ U = {"simple": "SimpleSGDUpdater", "squared_l2": "SquaredL2SGDUpdater", "l1": "L
      "adagrad": "AdaGradSGDUpdater", "adam": "AdamSGDUpdater"}
 
 
+def stateful_variant(upd, tol, nv):
+    """Kernel of a dense AdaGrad / Adam / L1 epoch: the feature-split chain_split (800 + 10 H +
+    NV, H = min(NV, 4) compute waves) for AdaGrad / Adam at tol = 0 from two row vectors on, else
+    the one-wave chain_dense (100 + NV)."""
+    if upd in ("adagrad", "adam") and tol == 0.0 and nv >= 2:
+        return 800 + 10 * min(nv, 4) + nv
+    return 100 + nv
+
+
 def data_for(pkg, oracle, case):
     offs = case["offsets"]
     P = len(offs) - 1
@@ -147,8 +156,8 @@ def test_dense_stateful_updaters(pkg, oracle, upd):
 @pytest.mark.parametrize("upd", ["adagrad", "adam", "l1"])
 @pytest.mark.parametrize("d,dtype", [(40, np.float64), (512, np.float32), (1024, np.float64), (2048, np.float32)])
 def test_dense_fp32_throughput_updaters(pkg, oracle, upd, d, dtype):
-    """AdaGrad / Adam / L1 in the fp32 throughput mode: chain_dense with the updater status in
-    registers (variant 10x), against the fp64 oracle at the fp32 tolerance, tol 0
+    """AdaGrad / Adam / L1 in the fp32 throughput mode: chain_dense / chain_split with the updater
+    status in registers (stateful_variant), against the fp64 oracle at the fp32 tolerance, tol 0
     and tol > 0 (per-sample breaks: counts may differ only when tol > 0)."""
     rng = np.random.default_rng(d + len(upd))
     n, P = 8000, 4
@@ -164,7 +173,7 @@ def test_dense_fp32_throughput_updaters(pkg, oracle, upd, d, dtype):
         nv = 1
         while nv * 64 * 16 // es < d:
             nv *= 2
-        assert pkg.optimization.get_context(0).last_kernel() == 100 + nv
+        assert pkg.optimization.get_context(0).last_kernel() == stateful_variant(upd, tol, nv)
         wr, hr, _ = oracle.run(oracle.Matrix(y, X.astype(np.float64)), offs, "logistic", upd, step, 3, reg,
                                np.zeros(d), tol=tol, n_threads=8)
         if tol > 0 and len(h) != len(hr):
@@ -486,8 +495,8 @@ def test_fp64_block_rows_in_registers(pkg, oracle, d, grad, upd, storage):
 @pytest.mark.parametrize("d,storage", [(40, np.float64), (300, np.float32), (1024, np.float32),
                                        (1024, np.float64)])
 def test_dense_fp64_stateful_updaters_in_registers(pkg, oracle, upd, d, storage):
-    """AdaGrad / Adam (SGDUpdater.scala:193-286) in the fp64 parity mode on chain_dense: the
-    weights and the updater status in registers (variant 10x, d <= 1,024), f32 and f64 rows,
+    """AdaGrad / Adam (SGDUpdater.scala:193-286) in the fp64 parity mode on chain_dense /
+    chain_split: the weights and the updater status in registers (stateful_variant), f32 and f64 rows,
     tol 0 and tol > 0 (per-sample breaks). 1e-9 and exact counts against the oracle."""
     rng = np.random.default_rng(d * 3 + len(upd))
     n, P = 2400, 4
@@ -502,7 +511,7 @@ def test_dense_fp64_stateful_updaters_in_registers(pkg, oracle, upd, d, storage)
     for tol in (0.0, 0.001):
         w, h, counts = pkg.runParallelizedSGD(data, pkg.LogisticGradient(), getattr(pkg, U[upd])(), step, 3,
                                               0.0, 1.0, np.zeros(d), tol, return_chain_counts=True)
-        assert pkg.optimization.get_context(0).last_kernel() == 100 + nv
+        assert pkg.optimization.get_context(0).last_kernel() == stateful_variant(upd, tol, nv)
         wr, hr, cr = oracle.run(oracle.Matrix(y, X.astype(np.float64)), offs, "logistic", upd, step, 3, 0.0,
                                 np.zeros(d), tol=tol, n_threads=8)
         tag = f"{upd} d={d} {np.dtype(storage).name} tol={tol}"

@@ -1,0 +1,107 @@
+"""chain_split (psgd_split.hip): the dense per-sample chain with its features split over H compute
+waves, the throughput kernel of AdaGrad / Adam (SGDUpdater.scala:193-286) at tol = 0.
+
+Every gradient x both updaters, f32 and f64 rows, full and ragged row vectors, H = 2 and 4, fp64
+compute at 1e-9 with exact counts against the oracle (ParallelizedSGD.scala:243-276), fp32
+compute at the fp32 tolerance; sampled batches (the loader's row-index path), 1-row and empty
+partitions."""
+import numpy as np
+import pytest
+
+from conftest import has_gpu
+from test_gpu_parity import FP32_LOSS_REL, FP32_REL, G, U, assert_close, stateful_variant
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not has_gpu():
+        pytest.skip("no GPU")
+
+
+def synth(rng, n, d, grad):
+    X = (rng.standard_normal((n, d)) / np.sqrt(d)).astype(np.float32)
+    w = rng.standard_normal(d)
+    z = X.astype(np.float64) @ w
+    if grad == "least_squares":
+        y = z + 0.1 * rng.standard_normal(n)
+    else:
+        y = (z + rng.logistic(size=n) > 0).astype(np.float64)
+    return X, y
+
+
+def nv_of(d, storage):
+    vec = 4 if storage == np.float32 else 2
+    nv = 1
+    while nv * 64 * vec < d:
+        nv *= 2
+    return nv
+
+
+def run_both(pkg, oracle, X, y, storage, P, grad, upd, step, compute="f64", frac=1.0, iters=3):
+    n, d = X.shape
+    data = pkg.PartitionedData.parallelize(y, X.astype(storage), P, dtype=storage)
+    offs = [i * n // P for i in range(P)] + [n]
+    w, h, counts = pkg.runParallelizedSGD(data, getattr(pkg, G[grad])(), getattr(pkg, U[upd])(), step, iters,
+                                          0.0, frac, np.zeros(d), 0.0, compute_dtype=compute,
+                                          return_chain_counts=True)
+    variant = pkg.optimization.get_context(0).last_kernel()
+    wr, hr, cr = oracle.run(oracle.Matrix(y, X.astype(np.float64)), offs, grad, upd, step, iters, 0.0,
+                            np.zeros(d), tol=0.0, fraction=frac, n_threads=8)
+    return w, h, counts, wr, hr, cr, variant
+
+
+@pytest.mark.parametrize("upd", ["adagrad", "adam"])
+@pytest.mark.parametrize("grad", ["logistic", "least_squares", "hinge"])
+@pytest.mark.parametrize("d,storage", [(300, np.float32), (700, np.float32), (1024, np.float32),
+                                       (2048, np.float32), (256, np.float64), (1000, np.float64)])
+def test_split_fp64_parity(pkg, oracle, grad, upd, d, storage):
+    rng = np.random.default_rng(d + 7 * len(grad) + len(upd))
+    X, y = synth(rng, 1600, d, grad)
+    w, h, counts, wr, hr, cr, variant = run_both(pkg, oracle, X, y, storage, 4, grad, upd, 0.1)
+    assert variant == stateful_variant(upd, 0.0, nv_of(d, storage)) and variant >= 800
+    tag = f"{grad} {upd} d={d} {np.dtype(storage).name}"
+    assert [list(c) for c in counts] == [list(c) for c in cr], tag
+    assert_close(w, wr, what=tag + " weights")
+    assert_close(h, hr, what=tag + " loss")
+
+
+@pytest.mark.parametrize("upd", ["adagrad", "adam"])
+@pytest.mark.parametrize("grad", ["logistic", "least_squares", "hinge"])
+@pytest.mark.parametrize("d", [700, 1024])
+def test_split_fp32(pkg, oracle, grad, upd, d):
+    rng = np.random.default_rng(d + 3 * len(grad) + len(upd))
+    X, y = synth(rng, 4000, d, grad)
+    w, h, counts, wr, hr, cr, variant = run_both(pkg, oracle, X, y, np.float32, 4, grad, upd, 0.05, compute="f32")
+    assert variant == 844
+    assert [list(c) for c in counts] == [list(c) for c in cr]
+    scale = np.max(np.abs(wr))
+    err = np.max(np.abs(w - wr)) / scale
+    assert err <= FP32_REL, f"{grad} {upd} d={d}: weights {err:.3g} x max|w|"
+    assert_close(h, hr, rel=FP32_LOSS_REL, what=f"{grad} {upd} d={d} fp32 loss")
+
+
+@pytest.mark.parametrize("upd", ["adagrad", "adam"])
+def test_split_sampled_batches(pkg, oracle, upd):
+    # miniBatchFraction < 1: the loader streams the sampled rows by index (PSGD.scala:242)
+    rng = np.random.default_rng(21)
+    X, y = synth(rng, 3000, 512, "logistic")
+    w, h, counts, wr, hr, cr, variant = run_both(pkg, oracle, X, y, np.float32, 3, "logistic", upd, 0.1, frac=0.4)
+    assert variant == 822
+    assert [list(c) for c in counts] == [list(c) for c in cr]
+    assert_close(w, wr, what="sampled weights")
+    assert_close(h, hr, what="sampled loss")
+
+
+@pytest.mark.parametrize("n,P", [(7, 5), (3, 5)])
+def test_split_tiny_and_empty_partitions(pkg, oracle, n, P):
+    # 1-row chains (no prefetch), and partitions with no rows (count 0, w_in)
+    rng = np.random.default_rng(n * P)
+    X, y = synth(rng, n, 600, "logistic")
+    for upd in ("adagrad", "adam"):
+        w, h, counts, wr, hr, cr, variant = run_both(pkg, oracle, X, y, np.float32, P, "logistic", upd, 0.5)
+        assert variant == 844
+        assert [list(c) for c in counts] == [list(c) for c in cr]
+        assert_close(w, wr, what=f"{upd} n={n} P={P} weights")
+        assert_close(h, hr, what=f"{upd} n={n} P={P} loss")

@@ -7,7 +7,7 @@ HBM bytes follow MI355X_MICROARCH.md §HBM: rocprofv3 reports FETCH_SIZE and WRI
 Read-scale rule (one rule for every summary, round 3 on): on gfx950 FETCH_SIZE counts exactly
 half the bytes of a wide (16 B/lane) coalesced streaming read (global_load and LDS-DMA alike);
 other access widths are uncalibrated. So a kernel whose reads are all 16-B/lane streams -- the
-dense chains (chain_block, chain_block64, chain_dense: LDS-DMA rows) and the folds -- gets
+dense chains (chain_block, chain_block64, chain_dense, chain_split: LDS-DMA rows) and the folds -- gets
 2 x FETCH_SIZE; every other kernel (the CSR chains: 4-B/lane entry loads and scattered 4/8-B
 gathers) gets FETCH_SIZE as counted (1 x), i.e. its gathers at the fabric-request granularity the
 counter reports. --read-scale overrides the rule for every kernel.
@@ -21,11 +21,11 @@ import os
 import statistics
 
 KERNELS = ("psgd::chain_block64", "psgd::chain_block", "psgd::chain_sparse_spec", "psgd::chain_sparse_lds", "psgd::chain_sparse",
-           "psgd::chain_dense", "psgd::chain_general", "psgd::fold_kernel", "psgd::fold_f32_kernel",
+           "psgd::chain_dense", "psgd::chain_split", "psgd::chain_general", "psgd::fold_kernel", "psgd::fold_f32_kernel",
            "psgd::wf32_init_kernel", "psgd::margin_loss_kernel", "psgd::logistic_loss64_kernel")
 
 
-STREAM_KERNELS = ("psgd::chain_block", "psgd::chain_dense", "psgd::fold_kernel", "psgd::fold_f32_kernel",
+STREAM_KERNELS = ("psgd::chain_block", "psgd::chain_dense", "psgd::chain_split", "psgd::fold_kernel", "psgd::fold_f32_kernel",
                   "psgd::wf32_init_kernel")
 
 
