@@ -47,6 +47,9 @@
 namespace psgd {
 
 constexpr int LCAP = 128;                  // entries per row (two per lane)
+#ifndef PSGD_LDS_EXP
+#define PSGD_LDS_EXP 0                     // cost probes (tools/r03_c4_probe.sh); 0 in the product
+#endif
 
 // The chain's tail gathers and stores are buffer instructions over its fp32 vector: a 32-bit
 // byte offset per lane, and lanes without a tail entry get an out-of-range offset, which the
@@ -489,7 +492,11 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
     };
     // Only tail entries touch memory: the other lanes get the no-access offset.
     auto gather = [&](const GCols& G, T (&g)[2]) __attribute__((always_inline)) {
+#if PSGD_LDS_EXP & 2   // experiment: the tail gathers read nothing (wrong results; cost probe)
+        const bool a0 = false, a1 = false;
+#else
         const bool a0 = lane < G.nnz && G.c0 >= K, a1 = lane + 64 < G.nnz && G.c1 >= K;
+#endif
         g[0] = buffer_gather_sc1(vrs, boff(a0, G.c0), T(0));
         g[1] = buffer_gather_sc1(vrs, boff(a1, G.c1), T(0));
     };
@@ -581,8 +588,13 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
         // this row's tail stores (2 VMEM instructions)
         if constexpr (TAIL) {
             const bool a0 = lane < cur.nnz && cur.c0 >= K, a1 = lane + 64 < cur.nnz && cur.c1 >= K;
+#if PSGD_LDS_EXP & 1   // experiment: the tail stores go nowhere (wrong results; cost probe)
+            buffer_store_f32(vrs, kNoAccess, nv0);
+            buffer_store_f32(vrs, kNoAccess, nv1);
+#else
             buffer_store_f32(vrs, boff(a0, cur.c0), nv0);
             buffer_store_f32(vrs, boff(a1, cur.c1), nv1);
+#endif
         }
         publish(&hdr->done, t + 1);
         cur = nxt;
