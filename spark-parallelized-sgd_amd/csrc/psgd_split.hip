@@ -1,10 +1,12 @@
 // psgd_split.hip -- the per-sample dense chain with the feature dimension split over H compute
-// waves (gfx950): the throughput kernel of the stateful updaters.
+// waves (gfx950): the throughput kernel of the updaters the blocked kernels do not take
+// (AdaGrad, Adam, L1).
 //
 // Reference (paths under /root/reference, src/main/scala/org/apache/spark/mllib/optimization/):
 //   chain loop      ParallelizedSGD.scala:243-270 (one chain per partition, per-sample updates)
 //   AdaGrad         SGDUpdater.scala:193-227  (status r += g*g; w += -s/sqrt(j) * g / (r + 1)^0.5)
 //   Adam            SGDUpdater.scala:238-286  (v, r; fix1 = (1 - r^iter)^0.5 + eps; lr = s / (1 - beta^iter))
+//   L1              SGDUpdater.scala:120-148  (soft thresholding: per coordinate, not a rank-1 step)
 //   gradients       [ext] MLlib 1.6.1 Gradient.scala (mult * x), as in psgd_kernels.hip
 //
 // AdaGrad / Adam keep per-feature status that depends non-linearly on each sample's gradient, so
@@ -354,6 +356,12 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
                     nw.x = old.x + a_s * (g.x * rsqrt_newton(acc2.x + T(1)));
                     nw.y = old.y + a_s * (g.y * rsqrt_newton(acc2.y + T(1)));
                 }
+            } else if constexpr (UPD == U_L1) {
+                // axpy(-s, grad, w), then soft thresholding by regParam * s (UPD.scala:133-146)
+                const T shrink = T(kp.reg) * s;
+                nw = old + a_s * (mult * x[e]);
+                nw.x = jsignum(nw.x) * jmax(T(0), m_fabs(nw.x) - shrink);
+                nw.y = jsignum(nw.y) * jmax(T(0), m_fabs(nw.y) - shrink);
             } else {
                 // Adam, the reference's variant: v = beta v + (1-beta) g, r = gamma r + (1-gamma) g^2,
                 // fix1 = sqrt(1 - r^iter) + eps, w += -lr * v / fix1
@@ -394,6 +402,19 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
     if (t < n && !stop) sample(std::integral_constant<int, 0>{}, t++);
     const int64_t count = t;   // n unless the chain stopped (then the host raises)
     if constexpr (sizeof(T) == 4) loss_sum += double(loss_blk);
+    // regVal of the chain's last update (PSGD.scala:257): AdaGrad / Adam 0.0 (UPD.scala:221, :266),
+    // L1 regParam * ||w||_1 (UPD.scala:147): the waves' partial norms through one more exchange
+    double rv = 0.0;
+    if constexpr (UPD == U_L1) {
+        if (n > 0) {
+            T acc = T(0);
+#pragma unroll
+            for (int e = 0; e < E; ++e) acc += m_fabs(w[e / 2][e % 2]);
+            publish(wave_sum_uniform(acc), n);
+            const T nrm = collect(n);
+            if (count > 0) rv = double(nrm) * kp.reg;
+        }
+    }
     PSGD_STAMP(if (L.stamps && lane == 0) {
         unsigned long long* o = L.stamps + (size_t)chain * 16 + 4 * h;
         o[0] = st_mark - st_begin;
@@ -415,7 +436,7 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
     if (h > 0) return;
     if constexpr (GRAD == G_LEAST_SQUARES) loss_sum = loss_sum / 2.0;
     if (lane == 0) {
-        L.rv[chain] = 0.0;   // AdaGrad / Adam return regVal 0.0 (UPD.scala:221, :266)
+        L.rv[chain] = rv;
         if constexpr (!ZOUT) L.loss[chain] = loss_sum;
         L.cnt[chain] = count;
         L.cnt_d[chain] = double(count);
@@ -488,6 +509,7 @@ int split_dispatch_upd(const ChainLaunch& L, const KParams& kp, int updater, int
                        size_t lds, hipStream_t st, int* variant) {
     if (updater == U_ADAGRAD) return split_dispatch_nv<S, T, GRAD, U_ADAGRAD>(L, kp, min_ld, max_ld, lds, st, variant);
     if (updater == U_ADAM) return split_dispatch_nv<S, T, GRAD, U_ADAM>(L, kp, min_ld, max_ld, lds, st, variant);
+    if (updater == U_L1) return split_dispatch_nv<S, T, GRAD, U_L1>(L, kp, min_ld, max_ld, lds, st, variant);
     return -3;
 }
 
@@ -506,7 +528,7 @@ int split_dispatch_grad(const ChainLaunch& L, const KParams& kp, int gradient, i
 
 bool split_path_applies(int layout, int updater, bool check_conv, int storage, int64_t max_ld) {
     if (layout != kDense || check_conv) return false;
-    if (updater != U_ADAGRAD && updater != U_ADAM) return false;
+    if (updater != U_ADAGRAD && updater != U_ADAM && updater != U_L1) return false;
     // PSGD_SPLIT=0 keeps chain_dense (A/B measurements)
     static const bool off = [] {
         const char* e = getenv("PSGD_SPLIT");

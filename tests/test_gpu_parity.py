@@ -44,9 +44,9 @@ U = {"simple": "SimpleSGDUpdater", "squared_l2": "SquaredL2SGDUpdater", "l1": "L
 
 def stateful_variant(upd, tol, nv):
     """Kernel of a dense AdaGrad / Adam / L1 epoch: the feature-split chain_split (800 + 10 H +
-    NV, H = min(NV, 4) compute waves) for AdaGrad / Adam at tol = 0 from two row vectors on, else
-    the one-wave chain_dense (100 + NV)."""
-    if upd in ("adagrad", "adam") and tol == 0.0 and nv >= 2:
+    NV, H = min(NV, 4) compute waves) at tol = 0 from two row vectors on, else the one-wave
+    chain_dense (100 + NV)."""
+    if upd in ("adagrad", "adam", "l1") and tol == 0.0 and nv >= 2:
         return 800 + 10 * min(nv, 4) + nv
     return 100 + nv
 

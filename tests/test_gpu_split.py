@@ -1,7 +1,7 @@
 """chain_split (psgd_split.hip): the dense per-sample chain with its features split over H compute
-waves, the throughput kernel of AdaGrad / Adam (SGDUpdater.scala:193-286) at tol = 0.
+waves, the throughput kernel of AdaGrad / Adam / L1 (SGDUpdater.scala:120-148, :193-286) at tol = 0.
 
-Every gradient x both updaters, f32 and f64 rows, full and ragged row vectors, H = 2 and 4, fp64
+Every gradient x the three updaters (L1 with regParam > 0), f32 and f64 rows, full and ragged row vectors, H = 2 and 4, fp64
 compute at 1e-9 with exact counts against the oracle (ParallelizedSGD.scala:243-276), fp32
 compute at the fp32 tolerance; sampled batches (the loader's row-index path), 1-row and empty
 partitions."""
@@ -41,18 +41,19 @@ def nv_of(d, storage):
 
 def run_both(pkg, oracle, X, y, storage, P, grad, upd, step, compute="f64", frac=1.0, iters=3):
     n, d = X.shape
+    reg = 0.002 if upd == "l1" else 0.0   # L1: the soft threshold and regVal = reg ||w||_1
     data = pkg.PartitionedData.parallelize(y, X.astype(storage), P, dtype=storage)
     offs = [i * n // P for i in range(P)] + [n]
     w, h, counts = pkg.runParallelizedSGD(data, getattr(pkg, G[grad])(), getattr(pkg, U[upd])(), step, iters,
-                                          0.0, frac, np.zeros(d), 0.0, compute_dtype=compute,
+                                          reg, frac, np.zeros(d), 0.0, compute_dtype=compute,
                                           return_chain_counts=True)
     variant = pkg.optimization.get_context(0).last_kernel()
-    wr, hr, cr = oracle.run(oracle.Matrix(y, X.astype(np.float64)), offs, grad, upd, step, iters, 0.0,
+    wr, hr, cr = oracle.run(oracle.Matrix(y, X.astype(np.float64)), offs, grad, upd, step, iters, reg,
                             np.zeros(d), tol=0.0, fraction=frac, n_threads=8)
     return w, h, counts, wr, hr, cr, variant
 
 
-@pytest.mark.parametrize("upd", ["adagrad", "adam"])
+@pytest.mark.parametrize("upd", ["adagrad", "adam", "l1"])
 @pytest.mark.parametrize("grad", ["logistic", "least_squares", "hinge"])
 @pytest.mark.parametrize("d,storage", [(300, np.float32), (700, np.float32), (1024, np.float32),
                                        (2048, np.float32), (256, np.float64), (1000, np.float64)])
@@ -67,7 +68,7 @@ def test_split_fp64_parity(pkg, oracle, grad, upd, d, storage):
     assert_close(h, hr, what=tag + " loss")
 
 
-@pytest.mark.parametrize("upd", ["adagrad", "adam"])
+@pytest.mark.parametrize("upd", ["adagrad", "adam", "l1"])
 @pytest.mark.parametrize("grad", ["logistic", "least_squares", "hinge"])
 @pytest.mark.parametrize("d", [700, 1024])
 def test_split_fp32(pkg, oracle, grad, upd, d):

@@ -20,6 +20,7 @@ declare -A ARGS=(
   [c3_f32_adam]="--workload c3 --updater adam"
   [c3_f64_adagrad]="--workload c3 --compute f64 --updater adagrad"
   [c3_f64_adam]="--workload c3 --compute f64 --updater adam"
+  [c1]="--workload c1 --compute f64"
 )
 NAMES=${@:-c2 c2_f64 c3_f32 c3_f64 c3_f64rows c4_f32 c4_f64 c5 c3_f32_adagrad c3_f32_adam c3_f64_adagrad c3_f64_adam}
 step() { echo "== $1"; shift; "$@"; rc=$?; echo "rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
