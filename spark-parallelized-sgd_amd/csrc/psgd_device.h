@@ -153,27 +153,43 @@ __device__ __forceinline__ float pow_fast(float a, float b) {
 }
 __device__ __forceinline__ float m_fma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 
-// 1/sqrt(x) for x >= 1 in f64: v_rsq_f64 and two Newton steps (x = inf gives 0, NaN stays NaN).
+// The fp64 kernels' reciprocals and square roots sit on per-sample dependent chains: the
+// hardware estimate and ONE Newton step. Measured on gfx950 (tools/newton_check, 4M inputs in
+// [1, 1e6)): v_rcp_f64 alone 4.6e-8 relative, + 1 Newton step 2.2e-15 (2 steps: exact);
+// v_rsq_f64 5.2e-8, + 1 step 4.3e-15 (2 steps: 2.6e-16) -- ~10-20 ulp, six orders of magnitude
+// inside the fp64 mode's 1e-9 bar, for two fewer dependent f64 operations (four for rsq).
+// 1/sqrt(x) for x >= 1 (x = inf gives 0, NaN stays NaN).
 __device__ __forceinline__ double rsqrt_newton(double x) {
     double y = __builtin_amdgcn_rsq(x);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const double e = __builtin_fma(-(x * y), y, 1.0);
-        y = __builtin_fma(0.5 * y, e, y);
-    }
+    const double e = __builtin_fma(-(x * y), y, 1.0);
+    y = __builtin_fma(0.5 * y, e, y);
     return x == __builtin_inf() ? 0.0 : y;
 }
+// 1/x for finite x != 0 (NaN stays NaN).
+__device__ __forceinline__ double recip_newton(double x) {
+    const double y = __builtin_amdgcn_rcp(x);
+    return __builtin_fma(y, __builtin_fma(-x, y, 1.0), y);
+}
+// sqrt(x) for x >= 0 as x * rsq(x) with one Newton step (sqrt(0) = 0, x < 0 or NaN gives NaN,
+// sqrt(inf) = inf).
+__device__ __forceinline__ double sqrt_newton(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    const double e = __builtin_fma(-(x * y), y, 1.0);
+    y = __builtin_fma(0.5 * y, e, y);
+    return (x == 0.0 || x == __builtin_inf()) ? x : x * y;
+}
 
-// pow(r, iter) of AdamSGDUpdater's fix1 (UPD.scala:262) for iter = j >= 1: when iter * log2(r) <
-// -1100 the power is below 2^-1100 and the library pow returns 0 (it rounds below half the
-// least denormal); the hardware f32 log2 (relative error ~1e-7, so the margin to 2^-1075 is
-// ~25 binades) decides that without the ~100-instruction f64 pow, which after a few hundred
-// samples no coordinate needs (r is an average of squared gradients, well below 1).
-__device__ __forceinline__ double pow_int_iter(double r, double iter) {
+// 1.0 - pow(r, iter), the inside of AdamSGDUpdater's fix1 (UPD.scala:262), iter = j >= 1,
+// bit for bit: when pow(r, iter) <= 2^-54 the f64 subtraction rounds 1 - p to exactly 1.0 (the
+// double below 1 is 1 - 2^-53), so the ~100-instruction f64 pow is needed only while
+// iter * log2(r) >= -60. The hardware f32 log2 (relative error ~1e-7: 6e-6 binades at 60) decides
+// that; the wave runs the pow only while one of its coordinates still needs it, i.e. for its
+// first few tens of samples (r is an average of squared gradients, well below 1).
+__device__ __forceinline__ double one_minus_pow_iter(double r, double iter) {
     const float l2 = __builtin_amdgcn_logf((float)r);
-    double p = 0.0;
-    if (!((float)iter * l2 < -1100.0f)) p = pow(r, iter);
-    return p;
+    double q = 1.0;
+    if (!((float)iter * l2 < -60.0f)) q = 1.0 - pow(r, iter);
+    return q;
 }
 
 // 1 / (1 + exp(m)) in f64 with a short dependent chain: the chains evaluate it once per row on
@@ -181,8 +197,8 @@ __device__ __forceinline__ double pow_int_iter(double r, double iter) {
 // div_fixup) are ~30 dependent f64 operations. Here: exp(m) = 2^k e^r, k = rint(m log2 e),
 // r = m - k ln2 (two-part ln2, |r| <= ln2/2), e^r by its Taylor polynomial of degree 13
 // (truncation < 2e-16 relative) evaluated Estrin-style (depth 5 instead of 13), 2^k by ldexp;
-// the reciprocal by v_rcp_f64 and two Newton steps. Within ~2 ulp of the reference's
-// 1.0 / (1.0 + exp(margin)) (the fp64 mode's bar is 1e-9 relative). m is clamped to
+// the reciprocal by v_rcp_f64 and one Newton step (above). Within ~1e-14 relative of the
+// reference's 1.0 / (1.0 + exp(margin)) (the fp64 mode's bar is 1e-9 relative). m is clamped to
 // [-746, 709] (exp(-746) is 0 in f64; beyond 709 the result is ~1e-308 instead of 0); a NaN
 // stays NaN.
 __device__ __forceinline__ double recip_one_plus_exp(double m) {
@@ -205,11 +221,7 @@ __device__ __forceinline__ double recip_one_plus_exp(double m) {
     const double q07 = __builtin_fma(r4, q47, q03);
     const double q8d = __builtin_fma(r4, pcd, q8b);
     const double er = __builtin_fma(r8, q8d, q07);
-    const double d = 1.0 + __builtin_amdgcn_ldexp(er, (int)kd);
-    double y = __builtin_amdgcn_rcp(d);
-    y = __builtin_fma(y, __builtin_fma(-d, y, 1.0), y);
-    y = __builtin_fma(y, __builtin_fma(-d, y, 1.0), y);
-    return y;
+    return recip_newton(1.0 + __builtin_amdgcn_ldexp(er, (int)kd));
 }
 
 // java.lang.Math.max(a, b): NaN if either is NaN.

@@ -338,7 +338,9 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
         T al = T(0);
         if constexpr (UPD == U_ADAM) {
             if constexpr (sizeof(T) == 4) al = -(s / (T(1) - pow_fast(T(kp.beta), iter)));
-            else al = -(s / (T(1) - m_pow(T(kp.beta), iter)));
+            // fp64: 1 - beta^iter as 1.0 once beta^iter <= 2^-54 (bit-identical, no library pow
+            // per sample on the chain) and the division by rcp + one Newton step
+            else al = -(s * recip_newton(one_minus_pow_iter(T(kp.beta), iter)));
         }
 #pragma unroll
         for (int e = 0; e < E2; ++e) {
@@ -379,10 +381,11 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
                     nw.x = old.x + al * (v.x * __builtin_amdgcn_rcpf(fx));
                     nw.y = old.y + al * (v.y * __builtin_amdgcn_rcpf(fy));
                 } else {
-                    const T fx = m_sqrt(T(1) - pow_int_iter(r.x, iter)) + T(kp.eps);
-                    const T fy = m_sqrt(T(1) - pow_int_iter(r.y, iter)) + T(kp.eps);
-                    nw.x = old.x + al * (v.x / fx);
-                    nw.y = old.y + al * (v.y / fy);
+                    // sqrt and v / fix1 by the hardware estimates + one Newton step (~1e-14)
+                    const T fx = sqrt_newton(one_minus_pow_iter(r.x, iter)) + T(kp.eps);
+                    const T fy = sqrt_newton(one_minus_pow_iter(r.y, iter)) + T(kp.eps);
+                    nw.x = old.x + al * (v.x * recip_newton(fx));
+                    nw.y = old.y + al * (v.y * recip_newton(fy));
                 }
             }
             w[e] = nw;

@@ -147,3 +147,42 @@ def test_two_ranks_match_single_process_oracle(tmp_path, oracle, pkg, P):
         np.testing.assert_allclose(res["h"], h, rtol=1e-14)
     else:
         assert np.array_equal(res["w"], w) and np.array_equal(res["h"], h)
+
+
+def _ckpt_worker(rank, world, port, ck, stop, result_path):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import __graft_entry__ as g
+    import oracle as O
+    pkg = g.load_package()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(21)
+        n, d = 400, 5
+        X = rng.standard_normal((n, d))
+        y = (rng.uniform(size=n) > 0.5).astype(float)
+        data = pkg.PartitionedData.parallelize(y, X, 4)
+        eng = make_oracle_engine(pkg, O)(data, rank, world)
+        w, h = pkg.runParallelizedSGD(data, pkg.LogisticGradient(), pkg.SquaredL2SGDUpdater(), 0.5, stop,
+                                      0.01, 1.0, np.zeros(d), 0.0, engine=eng, checkpoint=ck)
+        dist.barrier()   # rank 0's checkpoint is on disk before any rank resumes from it
+        if rank == 0 and result_path:
+            np.savez(result_path, w=w, h=h)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_checkpoint_resume(tmp_path):
+    """Checkpoint / resume with world size 2: rank 0 writes, every rank resumes from the file; the
+    resumed run equals the uninterrupted one bit for bit."""
+    world = 2
+    full, res = str(tmp_path / "full.npz"), str(tmp_path / "res.npz")
+    mp.start_processes(_ckpt_worker, args=(world, _free_port(), str(tmp_path / "a.npz"), 5, full),
+                       nprocs=world, start_method="spawn")
+    ck = str(tmp_path / "b.npz")
+    mp.start_processes(_ckpt_worker, args=(world, _free_port(), ck, 2, ""), nprocs=world, start_method="spawn")
+    mp.start_processes(_ckpt_worker, args=(world, _free_port(), ck, 5, res), nprocs=world, start_method="spawn")
+    a, b = np.load(full), np.load(res)
+    assert len(a["h"]) == 5 and np.array_equal(a["w"], b["w"]) and np.array_equal(a["h"], b["h"])

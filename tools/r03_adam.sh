@@ -1,0 +1,12 @@
+#!/bin/bash
+# Adam / AdaGrad GPU tests (golden cases included), then the c3 fp64 / fp32 Adam lines.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_gpu_split.py tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread 2>&1 | tail -3
+[ ${PIPESTATUS[0]} -eq 0 ] || exit 1
+B="python bench.py --secondary= --no-cpu-baseline --workload c3 --steps 3 --warmup 1"
+run() { echo "== $*"; timeout -k 10 200 "$@" > gpurun_out/_run.log 2>&1; rc=$?; grep -o '"avg_kernel_ms": [0-9.]*\|"kernel": "[^"(]*' gpurun_out/_run.log | tail -2 | tr '\n' ' '; echo; [ $rc -eq 0 ] || exit $rc; }
+run $B --updater adam --compute f64
+run $B --updater adam --compute f32
+run $B --updater adagrad --compute f64
