@@ -81,7 +81,13 @@ __device__ __forceinline__ uint64_t lds_read_u64(const uint64_t* p) {
     return v;
 }
 
-// fixed LDS area: [RingHeader 16 B][exchange 2 x H x PC u64][SIMD ids of the H + 1 waves]
+// RingHeader::stop values: the loader stops on any non-zero one; the compute waves' spins give up
+// only on an error (a watchdog), not on a per-sample convergence break, which every wave takes
+// at the same sample by itself.
+constexpr unsigned kStopError = 1u, kStopConverged = 2u;
+
+// fixed LDS area: [RingHeader 16 B][exchange 2 x H x W u64 (W words per wave and sample)]
+// [SIMD ids of the H + 1 waves]
 template <int H, int PC>
 constexpr size_t split_fixed_bytes() {
     return (sizeof(RingHeader) + 2 * H * PC * 8 + (H + 1) * 4 + 15) / 16 * 16;
@@ -89,7 +95,7 @@ constexpr size_t split_fixed_bytes() {
 
 }  // namespace
 
-template <typename S, typename T, int GRAD, int UPD, int NV, bool FULL, int H>
+template <typename S, typename T, int GRAD, int UPD, bool CONV, int NV, bool FULL, int H>
 __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KParams kp, RingGeom geom) {
     using V = typename Vec16<S>::type;
     constexpr int VEC = Vec16<S>::N;
@@ -98,7 +104,11 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
     constexpr int E2 = E / 2;
     constexpr int ROW_BYTES = NV * 1024;
     constexpr int PC = sizeof(T) / 4;        // 32-bit pieces of a partial
-    constexpr int XW = H * PC;               // exchange words per sample
+    // values a wave publishes per sample: its partial dot; with the per-sample convergence test
+    // (CONV, PSGD.scala:262) also its partial ||w_old - w_new||^2 and ||w_new||^2 of the previous
+    // sample, so the test of sample t - 1 rides on the exchange of sample t
+    constexpr int KV = CONV ? 3 : 1;
+    constexpr int XW = H * PC * KV;          // exchange words per sample
     static_assert(NV % H == 0 && E % 2 == 0, "the compute waves split the row vectors evenly");
     static_assert(XW <= 64, "one lane per exchange word");
     // Logistic: the per-row dots go to L.zbuf64 / L.zbuf, the losses are summed after the chain
@@ -107,7 +117,7 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
     RingHeader* hdr = reinterpret_cast<RingHeader*>(smem);
     uint64_t* xw = reinterpret_cast<uint64_t*>(smem + sizeof(RingHeader));
     unsigned* simd_of = reinterpret_cast<unsigned*>(xw + 2 * XW);
-    char* meta_ring = smem + split_fixed_bytes<H, PC>();
+    char* meta_ring = smem + split_fixed_bytes<H, PC * KV>();
     char* ring = meta_ring + geom.meta_blocks * kMetaBlockBytes;
 
     const int lane = threadIdx.x & 63;
@@ -197,7 +207,7 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
                 if (__hip_atomic_load(&hdr->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) { stop = true; break; }
                 if (__builtin_amdgcn_s_memrealtime() - t0 > kWatchdogTicks) {
                     __hip_atomic_fetch_or(L.watchdog, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_store(&hdr->stop, kStopError, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     stop = true;
                     break;
                 }
@@ -206,23 +216,28 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
         }
     };
 
-    // The exchange of sample t: publish writes this wave's partial (lanes 0 .. PC-1, one word
-    // each); collect polls the XW words of the parity slot (lane l reads word l) until all carry
-    // the sample's tag and returns their sum in wave order. A stopped chain leaves collect with
-    // whatever it read (the host raises on the watchdog word).
+    // The exchange of sample t: publish writes this wave's KV values (lane l < PC KV writes word
+    // l: value l / PC, 32-bit piece l % PC); collect polls the XW words of the parity slot (lane l
+    // reads word l) until all carry the sample's tag and returns each value summed over the waves
+    // in wave order. A stopped chain leaves collect with whatever it read (the host raises on the
+    // watchdog word).
     constexpr uint64_t kMask = XW == 64 ? ~0ull : ((1ull << XW) - 1);
-    auto publish = [&](T zh, int64_t t) __attribute__((always_inline)) {
+    auto publish = [&](const T (&val)[KV], int64_t t) __attribute__((always_inline)) {
+        const int k = lane / PC;
+        T vk = val[0];
+#pragma unroll
+        for (int q = 1; q < KV; ++q) vk = k == q ? val[q] : vk;
         uint32_t piece;
         if constexpr (PC == 1) {
-            piece = __float_as_uint(zh);
+            piece = __float_as_uint(vk);
         } else {
-            const uint64_t b = (uint64_t)__double_as_longlong(zh);
-            piece = lane == 0 ? (uint32_t)b : (uint32_t)(b >> 32);
+            const uint64_t b = (uint64_t)__double_as_longlong(vk);
+            piece = (lane & 1) == 0 ? (uint32_t)b : (uint32_t)(b >> 32);
         }
-        if (lane < PC)
-            lds_write_u64(xw + (int)(t & 1) * XW + h * PC + lane, ((uint64_t)(uint32_t)(t + 1) << 32) | piece);
+        if (lane < PC * KV)
+            lds_write_u64(xw + (int)(t & 1) * XW + h * PC * KV + lane, ((uint64_t)(uint32_t)(t + 1) << 32) | piece);
     };
-    auto collect = [&](int64_t t) __attribute__((always_inline)) -> T {
+    auto collect = [&](int64_t t, T (&sum)[KV]) __attribute__((always_inline)) {
         const uint32_t tag = (uint32_t)(t + 1);
         const uint64_t* src = xw + (int)(t & 1) * XW + (lane < XW ? lane : 0);
         uint64_t v = lds_read_u64(src);
@@ -234,12 +249,12 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
                 v = lds_read_u64(src);
                 if ((__ballot((uint32_t)(v >> 32) == tag) & kMask) == kMask) break;
                 if ((spin & 1023) == 0) {
-                    if (__hip_atomic_load(&hdr->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) { stop = true; break; }
+                    if (__hip_atomic_load(&hdr->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == kStopError) { stop = true; break; }
                     const uint64_t now = __builtin_amdgcn_s_memrealtime();
                     if (t0 == 0) t0 = now;
                     if (now - t0 > kWatchdogTicks) {
                         __hip_atomic_fetch_or(L.watchdog, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_store(&hdr->stop, kStopError, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         stop = true;
                         break;
                     }
@@ -247,20 +262,24 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
             }
         }
         const int lo = (int)(uint32_t)v;
-        T acc = T(0);
 #pragma unroll
-        for (int g = 0; g < H; ++g) {
-            T pg;
-            if constexpr (PC == 1) {
-                pg = __int_as_float(__builtin_amdgcn_readlane(lo, g));
-            } else {
-                const uint32_t a = (uint32_t)__builtin_amdgcn_readlane(lo, 2 * g);
-                const uint32_t b = (uint32_t)__builtin_amdgcn_readlane(lo, 2 * g + 1);
-                pg = __longlong_as_double((long long)(((uint64_t)b << 32) | a));
+        for (int q = 0; q < KV; ++q) {
+            T acc = T(0);
+#pragma unroll
+            for (int g = 0; g < H; ++g) {
+                const int wd = g * PC * KV + q * PC;
+                T pg;
+                if constexpr (PC == 1) {
+                    pg = __int_as_float(__builtin_amdgcn_readlane(lo, wd));
+                } else {
+                    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane(lo, wd);
+                    const uint32_t b = (uint32_t)__builtin_amdgcn_readlane(lo, wd + 1);
+                    pg = __longlong_as_double((long long)(((uint64_t)b << 32) | a));
+                }
+                acc = g == 0 ? pg : acc + pg;
             }
-            acc = g == 0 ? pg : acc + pg;
+            sum[q] = acc;
         }
-        return acc;
     };
 
     double loss_sum = 0.0;
@@ -272,6 +291,10 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
     }
     const char* slot_ptr = ring;
     const char* const ring_end = ring + geom.rows * ROW_BYTES;
+    // CONV: this wave's ||w_old - w_new||^2, ||w_new||^2 of the last update (wave-reduced), the
+    // sample at which the test of its predecessor broke the chain (n: no break)
+    T pdsq = T(0), pnsq = T(0);
+    int64_t conv_at = n;
 
     // diagnostic builds (-DPSGD_STAMPS): cycles per phase of this wave's samples
     PSGD_STAMP(uint64_t st_dot = 0, st_x = 0, st_upd = 0; const uint64_t st_begin = __builtin_amdgcn_s_memtime();
@@ -293,7 +316,12 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
             if (e + 1 < E2) a1 = __builtin_elementwise_fma(x[e + 1], w[e + 1], a1);
         }
         const T2 a = a0 + a1;
-        publish(wave_sum_uniform(a.x + a.y), t);
+        {
+            T val[KV];
+            val[0] = wave_sum_uniform(a.x + a.y);
+            if constexpr (CONV) { val[1] = pdsq; val[2] = pnsq; }
+            publish(val, t);
+        }
         SPLIT_STAMP(st_dot);
 
         const char* next_ptr = slot_ptr + ROW_BYTES;
@@ -302,8 +330,21 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
         read_row(std::integral_constant<int, 1 - p>{}, next_ptr, t + 1);   // past the end: unused
         slot_ptr = next_ptr;
 
-        const T z = collect(t);
+        T sums[KV];
+        collect(t, sums);
+        const T z = sums[0];
         SPLIT_STAMP(st_x);
+        if constexpr (CONV) {
+            // isConverged(old, new, tol) of sample t - 1 (PSGD.scala:262, :333-335): the chain
+            // breaks after it -- sample t is not taken (no update, loss or count)
+            if (t > 0 && m_sqrt(sums[1]) < T(kp.tol) * jmax(m_sqrt(sums[2]), T(1))) {
+                conv_at = t;
+                // the loader stops refilling (kStopConverged: not an error -- the waves' spins
+                // give up only on kStopError)
+                if (h == 0) __hip_atomic_store(&hdr->stop, kStopConverged, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                return;
+            }
+        }
         if (h == 0 && ((t & 1) == 1 || t + 1 == n)) {
             // every wave has published sample t, so every wave has read rows <= t + 1
             __hip_atomic_store(&hdr->consumed, (unsigned)(t + 1), __ATOMIC_RELAXED,
@@ -342,6 +383,7 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
             // per sample on the chain) and the division by rcp + one Newton step
             else al = -(s * recip_newton(one_minus_pow_iter(T(kp.beta), iter)));
         }
+        T2 dsq2 = T2{T(0), T(0)}, nsq2 = T2{T(0), T(0)};
 #pragma unroll
         for (int e = 0; e < E2; ++e) {
             const T2 old = w[e];
@@ -358,6 +400,13 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
                     nw.x = old.x + a_s * (g.x * rsqrt_newton(acc2.x + T(1)));
                     nw.y = old.y + a_s * (g.y * rsqrt_newton(acc2.y + T(1)));
                 }
+            } else if constexpr (UPD == U_SQUARED_L2) {
+                const T c = T(1) - s * T(kp.reg);
+                nw = old * c;                       // brzWeights :*= (1 - s*lambda) (UPD.scala:172)
+                nw = nw + a_s * (mult * x[e]);      // axpy(-s, grad, w)
+            } else if constexpr (UPD == U_SIMPLE) {
+                if constexpr (sizeof(T) == 4) nw = __builtin_elementwise_fma(T2{a_s * mult, a_s * mult}, x[e], old);
+                else nw = old + a_s * (mult * x[e]);   // the reference's two roundings (UPD.scala:95)
             } else if constexpr (UPD == U_L1) {
                 // axpy(-s, grad, w), then soft thresholding by regParam * s (UPD.scala:133-146)
                 const T shrink = T(kp.reg) * s;
@@ -389,6 +438,11 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
                 }
             }
             w[e] = nw;
+            if constexpr (CONV) { const T2 df = old - nw; dsq2 += df * df; nsq2 += nw * nw; }
+        }
+        if constexpr (CONV) {
+            pdsq = wave_sum_uniform(dsq2.x + dsq2.y);
+            pnsq = wave_sum_uniform(nsq2.x + nsq2.y);
         }
         SPLIT_STAMP(st_upd);
     };
@@ -398,24 +452,41 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
         read_row(std::integral_constant<int, 0>{}, ring, 0);
     }
     int64_t t = 0;
-    for (; t + 2 <= n && !stop; t += 2) {
+    for (; t + 2 <= n && !stop && conv_at == n; t += 2) {
         sample(std::integral_constant<int, 0>{}, t);
+        if (conv_at < n) break;
         sample(std::integral_constant<int, 1>{}, t + 1);
     }
-    if (t < n && !stop) sample(std::integral_constant<int, 0>{}, t++);
-    const int64_t count = t;   // n unless the chain stopped (then the host raises)
+    if (t < n && !stop && conv_at == n) sample(std::integral_constant<int, 0>{}, t++);
+    // the samples taken: n, or up to the per-sample break (a stopped chain: the host raises)
+    const int64_t count = conv_at < n ? conv_at : t;
     if constexpr (sizeof(T) == 4) loss_sum += double(loss_blk);
-    // regVal of the chain's last update (PSGD.scala:257): AdaGrad / Adam 0.0 (UPD.scala:221, :266),
-    // L1 regParam * ||w||_1 (UPD.scala:147): the waves' partial norms through one more exchange
+    // regVal of the chain's last update (PSGD.scala:257): Simple / AdaGrad / Adam 0.0
+    // (UPD.scala:97, :221, :266), L1 regParam * ||w||_1 (:147), SquaredL2 0.5 regParam ||w||^2
+    // (:180): the waves' partial norms through one more exchange
     double rv = 0.0;
-    if constexpr (UPD == U_L1) {
+    if constexpr (UPD == U_L1 || UPD == U_SQUARED_L2) {
         if (n > 0) {
             T acc = T(0);
 #pragma unroll
-            for (int e = 0; e < E; ++e) acc += m_fabs(w[e / 2][e % 2]);
-            publish(wave_sum_uniform(acc), n);
-            const T nrm = collect(n);
-            if (count > 0) rv = double(nrm) * kp.reg;
+            for (int e = 0; e < E; ++e) {
+                const T we = w[e / 2][e % 2];
+                if constexpr (UPD == U_L1) acc += m_fabs(we);
+                else acc += we * we;
+            }
+            T val[KV], nrm[KV];
+            val[0] = wave_sum_uniform(acc);
+            if constexpr (CONV) { val[1] = T(0); val[2] = T(0); }
+            publish(val, n);
+            collect(n, nrm);
+            if (count > 0) {
+                if constexpr (UPD == U_L1) {
+                    rv = double(nrm[0]) * kp.reg;
+                } else {
+                    const double r2 = sqrt(double(nrm[0]));
+                    rv = 0.5 * kp.reg * r2 * r2;
+                }
+            }
         }
     }
     PSGD_STAMP(if (L.stamps && lane == 0) {
@@ -459,10 +530,10 @@ int split_nv(int64_t max_ld) {
     return nv;
 }
 
-template <typename S, typename T, int GRAD, int UPD, int NV>
+template <typename S, typename T, int GRAD, int UPD, bool CONV, int NV>
 int launch_split(const ChainLaunch& L, const KParams& kp, bool full, size_t lds, hipStream_t st) {
     constexpr int H = NV < PSGD_SPLIT_HMAX ? NV : PSGD_SPLIT_HMAX;
-    constexpr int PC = sizeof(T) / 4;
+    constexpr int PC = sizeof(T) / 4 * (CONV ? 3 : 1);   // 32-bit words per wave and sample
     constexpr int ROW = NV * 1024;
     constexpr size_t FIX = split_fixed_bytes<H, PC>();
     const size_t budget = lds > 0 ? lds : (size_t)64 * 1024;
@@ -480,7 +551,7 @@ int launch_split(const ChainLaunch& L, const KParams& kp, bool full, size_t lds,
     }
     RingGeom g{R, MB, D, 0};
     const size_t bytes = FIX + (size_t)MB * kMetaBlockBytes + (size_t)R * ROW;
-    auto k = full ? chain_split<S, T, GRAD, UPD, NV, true, H> : chain_split<S, T, GRAD, UPD, NV, false, H>;
+    auto k = full ? chain_split<S, T, GRAD, UPD, CONV, NV, true, H> : chain_split<S, T, GRAD, UPD, CONV, NV, false, H>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(64 * (H + 1)), bytes, st, L, kp, g);
     if constexpr (GRAD == G_LOGISTIC) {
@@ -492,7 +563,7 @@ int launch_split(const ChainLaunch& L, const KParams& kp, bool full, size_t lds,
     return (int)hipGetLastError();
 }
 
-template <typename S, typename T, int GRAD, int UPD>
+template <typename S, typename T, int GRAD, int UPD, bool CONV>
 int split_dispatch_nv(const ChainLaunch& L, const KParams& kp, int64_t min_ld, int64_t max_ld, size_t lds,
                       hipStream_t st, int* variant) {
     constexpr int VEC = 16 / sizeof(S);
@@ -500,20 +571,35 @@ int split_dispatch_nv(const ChainLaunch& L, const KParams& kp, int64_t min_ld, i
     const bool full = min_ld >= (int64_t)nv * 64 * VEC;
     if (variant) *variant = 800 + 10 * (nv < PSGD_SPLIT_HMAX ? nv : PSGD_SPLIT_HMAX) + nv;
     switch (nv) {
-    case 2: return launch_split<S, T, GRAD, UPD, 2>(L, kp, full, lds, st);
-    case 4: return launch_split<S, T, GRAD, UPD, 4>(L, kp, full, lds, st);
-    case 8: return launch_split<S, T, GRAD, UPD, 8>(L, kp, full, lds, st);
+    case 2: return launch_split<S, T, GRAD, UPD, CONV, 2>(L, kp, full, lds, st);
+    case 4: return launch_split<S, T, GRAD, UPD, CONV, 4>(L, kp, full, lds, st);
+    case 8: return launch_split<S, T, GRAD, UPD, CONV, 8>(L, kp, full, lds, st);
     default: return -3;
     }
+}
+
+template <typename S, typename T, int GRAD, bool CONV>
+int split_dispatch_conv(const ChainLaunch& L, const KParams& kp, int updater, int64_t min_ld, int64_t max_ld,
+                        size_t lds, hipStream_t st, int* variant) {
+    switch (updater) {
+    case U_ADAGRAD: return split_dispatch_nv<S, T, GRAD, U_ADAGRAD, CONV>(L, kp, min_ld, max_ld, lds, st, variant);
+    case U_ADAM: return split_dispatch_nv<S, T, GRAD, U_ADAM, CONV>(L, kp, min_ld, max_ld, lds, st, variant);
+    case U_L1: return split_dispatch_nv<S, T, GRAD, U_L1, CONV>(L, kp, min_ld, max_ld, lds, st, variant);
+    default: break;
+    }
+    if constexpr (CONV) {   // tol = 0 keeps the blocked kernels for these two
+        if (updater == U_SIMPLE) return split_dispatch_nv<S, T, GRAD, U_SIMPLE, true>(L, kp, min_ld, max_ld, lds, st, variant);
+        if (updater == U_SQUARED_L2) return split_dispatch_nv<S, T, GRAD, U_SQUARED_L2, true>(L, kp, min_ld, max_ld, lds, st, variant);
+    }
+    return -3;
 }
 
 template <typename S, typename T, int GRAD>
 int split_dispatch_upd(const ChainLaunch& L, const KParams& kp, int updater, int64_t min_ld, int64_t max_ld,
                        size_t lds, hipStream_t st, int* variant) {
-    if (updater == U_ADAGRAD) return split_dispatch_nv<S, T, GRAD, U_ADAGRAD>(L, kp, min_ld, max_ld, lds, st, variant);
-    if (updater == U_ADAM) return split_dispatch_nv<S, T, GRAD, U_ADAM>(L, kp, min_ld, max_ld, lds, st, variant);
-    if (updater == U_L1) return split_dispatch_nv<S, T, GRAD, U_L1>(L, kp, min_ld, max_ld, lds, st, variant);
-    return -3;
+    // the per-sample convergence test runs exactly when tol > 0 (psgd_capi.cpp: check_conv)
+    if (kp.tol > 0.0) return split_dispatch_conv<S, T, GRAD, true>(L, kp, updater, min_ld, max_ld, lds, st, variant);
+    return split_dispatch_conv<S, T, GRAD, false>(L, kp, updater, min_ld, max_ld, lds, st, variant);
 }
 
 template <typename S, typename T>
@@ -530,8 +616,10 @@ int split_dispatch_grad(const ChainLaunch& L, const KParams& kp, int gradient, i
 }  // namespace
 
 bool split_path_applies(int layout, int updater, bool check_conv, int storage, int64_t max_ld) {
-    if (layout != kDense || check_conv) return false;
-    if (updater != U_ADAGRAD && updater != U_ADAM && updater != U_L1) return false;
+    if (layout != kDense) return false;
+    // AdaGrad / Adam / L1 always; Simple / SquaredL2 with the per-sample convergence test (at
+    // tol = 0 the blocked kernels take them)
+    if (updater != U_ADAGRAD && updater != U_ADAM && updater != U_L1 && !check_conv) return false;
     // PSGD_SPLIT=0 keeps chain_dense (A/B measurements)
     static const bool off = [] {
         const char* e = getenv("PSGD_SPLIT");
@@ -545,7 +633,7 @@ bool split_path_applies(int layout, int updater, bool check_conv, int storage, i
 int launch_split_chains(const ChainLaunch& L, const KParams& kp, int storage, int compute, int gradient,
                         int updater, int64_t min_ld, int64_t max_ld, int lds_spread, hipStream_t st,
                         int* variant) {
-    if (!split_path_applies(kDense, updater, false, storage, max_ld)) return -3;
+    if (!split_path_applies(kDense, updater, kp.tol > 0.0, storage, max_ld)) return -3;
     const size_t lds = (size_t)(lds_spread > 0 ? lds_spread : 0);
     if (storage == 1) {
         if (compute == 1) return split_dispatch_grad<float, float>(L, kp, gradient, updater, min_ld, max_ld, lds, st, variant);

@@ -43,10 +43,10 @@ U = {"simple": "SimpleSGDUpdater", "squared_l2": "SquaredL2SGDUpdater", "l1": "L
 
 
 def stateful_variant(upd, tol, nv):
-    """Kernel of a dense AdaGrad / Adam / L1 epoch: the feature-split chain_split (800 + 10 H +
-    NV, H = min(NV, 4) compute waves) at tol = 0 from two row vectors on, else the one-wave
-    chain_dense (100 + NV)."""
-    if upd in ("adagrad", "adam", "l1") and tol == 0.0 and nv >= 2:
+    """Kernel of a dense per-sample epoch (AdaGrad / Adam / L1 at any tol, every updater at
+    tol > 0): the feature-split chain_split (800 + 10 H + NV, H = min(NV, 4) compute waves) from
+    two row vectors on, else the one-wave chain_dense (100 + NV)."""
+    if (upd in ("adagrad", "adam", "l1") or tol > 0.0) and nv >= 2:
         return 800 + 10 * min(nv, 4) + nv
     return 100 + nv
 
@@ -186,13 +186,13 @@ def test_dense_fp32_throughput_updaters(pkg, oracle, upd, d, dtype):
 
 def test_kernel_selection(pkg, oracle):
     """fp64 compute: tol = 0 with Simple/SquaredL2 runs the blocked fp64 kernel (70x one chain
-    wave, 71x two), tol > 0 the per-sample chain_dense (10x), d past the register-resident range
-    chain_general (200)."""
+    wave, 71x two), tol > 0 the per-sample kernels (chain_dense 10x for one row vector,
+    chain_split 8xx from two), d past the register-resident range chain_general (200)."""
     rng = np.random.default_rng(1)
     for d, dtype, tol, expect in ((100, np.float64, 0.0, 701), (512, np.float32, 0.0, 712),
                                   (1024, np.float32, 0.0, 714), (2048, np.float32, 0.0, 718),
                                   (1024, np.float64, 0.0, 718),
-                                  (100, np.float64, 0.001, 101), (512, np.float32, 0.001, 102),
+                                  (100, np.float64, 0.001, 101), (512, np.float32, 0.001, 822),
                                   (3000, np.float64, 0.0, 200)):
         X, y = synth(rng, 64, d, "logistic", dtype)
         data = pkg.PartitionedData.parallelize(y, X, 2, dtype=dtype)

@@ -106,3 +106,29 @@ def test_split_tiny_and_empty_partitions(pkg, oracle, n, P):
         assert [list(c) for c in counts] == [list(c) for c in cr]
         assert_close(w, wr, what=f"{upd} n={n} P={P} weights")
         assert_close(h, hr, what=f"{upd} n={n} P={P} loss")
+
+
+@pytest.mark.parametrize("upd", ["simple", "squared_l2", "l1", "adagrad", "adam"])
+@pytest.mark.parametrize("grad", ["logistic", "least_squares", "hinge"])
+@pytest.mark.parametrize("d,storage,tol", [(700, np.float32, 0.002), (1024, np.float32, 0.02),
+                                           (256, np.float64, 0.005)])
+def test_split_per_sample_convergence(pkg, oracle, grad, upd, d, storage, tol):
+    """tol > 0: the per-sample isConverged break (PSGD.scala:262, :324-336) on chain_split, its
+    test of sample t - 1 carried by the exchange of sample t; every updater (Simple / SquaredL2
+    take this kernel only with the test). fp64 at 1e-9 with exact per-chain counts."""
+    rng = np.random.default_rng(d + 11 * len(grad) + 5 * len(upd))
+    X, y = synth(rng, 2400, d, grad)
+    n = X.shape[0]
+    P = 4
+    reg = {"l1": 0.002, "squared_l2": 0.05}.get(upd, 0.0)
+    data = pkg.PartitionedData.parallelize(y, X.astype(storage), P, dtype=storage)
+    offs = [i * n // P for i in range(P)] + [n]
+    w, h, counts = pkg.runParallelizedSGD(data, getattr(pkg, G[grad])(), getattr(pkg, U[upd])(), 0.2, 3,
+                                          reg, 1.0, np.zeros(d), tol, return_chain_counts=True)
+    assert pkg.optimization.get_context(0).last_kernel() == stateful_variant(upd, tol, nv_of(d, storage))
+    wr, hr, cr = oracle.run(oracle.Matrix(y, X.astype(np.float64)), offs, grad, upd, 0.2, 3, reg,
+                            np.zeros(d), tol=tol, n_threads=8)
+    tag = f"{grad} {upd} d={d} tol={tol}"
+    assert [list(c) for c in counts] == [list(c) for c in cr[: len(counts)]], tag
+    assert_close(w, wr, what=tag + " weights")
+    assert_close(h, hr, what=tag + " loss")
