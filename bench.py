@@ -69,9 +69,9 @@ def pmc_traffic(workload, grad, variant, storage, rows, compute="f32", updater="
     if variant < 200:   # chain_dense<S, T, GRAD, UPD, CONV = false, NV, FULL>
         cname = "float" if compute == "f32" else "double"
         prefix = f"psgd::chain_dense<{sname}, {cname}, {g}, {u}, false, {variant - 100},"
-    elif variant >= 800:   # chain_split<S, T, GRAD, UPD, NV, FULL, H>
+    elif variant >= 800:   # chain_split<S, T, GRAD, UPD, CONV = false, NV, FULL, H>
         cname = "float" if compute == "f32" else "double"
-        prefix = f"psgd::chain_split<{sname}, {cname}, {g}, {u}, {variant % 10},"
+        prefix = f"psgd::chain_split<{sname}, {cname}, {g}, {u}, false, {variant % 10},"
     elif variant >= 700:
         prefix = f"psgd::chain_block64<{sname}, {g}, {u}, {variant % 10}, "
         waves = 1 + (variant - 700) // 10
