@@ -8,6 +8,7 @@
 // usage: psgd_run <file.libsvm> [--partitions P] [--features D] [--gradient logistic|
 //        least_squares|hinge] [--updater simple|squared_l2|l1|adagrad|adam] [--step S]
 //        [--iterations N] [--reg R] [--fraction F] [--tol T] [--compute f64|f32] [--device K]
+//        [--checkpoint FILE]
 #include "../../include/psgd.h"
 
 #include <chrono>
@@ -65,6 +66,68 @@ void print_array(const char* name, const double* v, size_t n, bool last = false)
     std::printf(last ? "]" : "], ");
 }
 
+// Checkpoint of the driver loop (--checkpoint FILE; the Python host's DriverCheckpoint): the
+// state between iterations -- next iteration, regVal, whether currentWeights is set, converged,
+// the loss history and the weights -- behind a fingerprint of the parameters and the data shape
+// (numIterations excluded: a finished run can be continued with a larger budget). Written after
+// every iteration to FILE.tmp and renamed over FILE.
+struct LoopState {
+    int32_t i = 1;
+    double regVal = 0.0;
+    int32_t have_current = 0, converged = 0;
+    std::vector<double> history, weights;
+};
+constexpr char kCkptMagic[8] = {'P', 'S', 'G', 'D', 'C', 'K', '0', '1'};
+
+std::vector<double> ckpt_fingerprint(const psgd_params& p, int64_t rows, int32_t parts, int32_t d) {
+    return {(double)p.gradient, (double)p.updater, (double)p.compute_dtype, p.step_size, p.reg_param,
+            p.mini_batch_fraction, p.convergence_tol, p.adam_beta, p.adam_gamma, p.adam_eps,
+            (double)p.num_classes, (double)rows, (double)parts, (double)d};
+}
+
+bool ckpt_save(const std::string& path, const std::vector<double>& fp, const LoopState& st) {
+    const std::string tmp = path + ".tmp";
+    FILE* f = std::fopen(tmp.c_str(), "wb");
+    if (!f) return false;
+    const uint64_t nf = fp.size(), nh = st.history.size(), nw = st.weights.size();
+    bool ok = std::fwrite(kCkptMagic, 1, 8, f) == 8 && std::fwrite(&nf, 8, 1, f) == 1 &&
+              std::fwrite(fp.data(), 8, nf, f) == nf && std::fwrite(&st.i, 4, 1, f) == 1 &&
+              std::fwrite(&st.regVal, 8, 1, f) == 1 && std::fwrite(&st.have_current, 4, 1, f) == 1 &&
+              std::fwrite(&st.converged, 4, 1, f) == 1 && std::fwrite(&nh, 8, 1, f) == 1 &&
+              std::fwrite(st.history.data(), 8, nh, f) == nh && std::fwrite(&nw, 8, 1, f) == 1 &&
+              std::fwrite(st.weights.data(), 8, nw, f) == nw;
+    ok = (std::fclose(f) == 0) && ok;
+    return ok && std::rename(tmp.c_str(), path.c_str()) == 0;
+}
+
+// 1: resumed, 0: no file, -1: unreadable or of other parameters / data
+int ckpt_load(const std::string& path, const std::vector<double>& fp, int32_t d, LoopState& st) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) return 0;
+    char magic[8];
+    uint64_t nf = 0, nh = 0, nw = 0;
+    std::vector<double> got;
+    bool ok = std::fread(magic, 1, 8, f) == 8 && std::memcmp(magic, kCkptMagic, 8) == 0 &&
+              std::fread(&nf, 8, 1, f) == 1 && nf == fp.size();
+    if (ok) {
+        got.resize(nf);
+        ok = std::fread(got.data(), 8, nf, f) == nf && got == fp && std::fread(&st.i, 4, 1, f) == 1 &&
+             std::fread(&st.regVal, 8, 1, f) == 1 && std::fread(&st.have_current, 4, 1, f) == 1 &&
+             std::fread(&st.converged, 4, 1, f) == 1 && std::fread(&nh, 8, 1, f) == 1 && nh < (1u << 30);
+    }
+    if (ok) {
+        st.history.resize(nh);
+        ok = std::fread(st.history.data(), 8, nh, f) == nh && std::fread(&nw, 8, 1, f) == 1 &&
+             nw == (uint64_t)d;
+    }
+    if (ok) {
+        st.weights.resize(nw);
+        ok = std::fread(st.weights.data(), 8, nw, f) == nw;
+    }
+    std::fclose(f);
+    return ok ? 1 : -1;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -77,6 +140,7 @@ int main(int argc, char** argv) {
     static const char* const kUpd[] = {"simple", "squared_l2", "l1", "adagrad", "adam"};
     static const char* const kDt[] = {"f64", "f32"};
     int parts = 2, features = -1, device = 0, iterations = 100;
+    std::string checkpoint;
     psgd_params p{};
     p.gradient = PSGD_GRADIENT_LOGISTIC;
     p.updater = PSGD_UPDATER_SIMPLE;
@@ -103,6 +167,7 @@ int main(int argc, char** argv) {
         else if (k == "--reg") p.reg_param = std::atof(v);
         else if (k == "--fraction") p.mini_batch_fraction = std::atof(v);
         else if (k == "--tol") p.convergence_tol = std::atof(v);
+        else if (k == "--checkpoint") checkpoint = v;
         else {
             std::fprintf(stderr, "psgd_run: unknown option %s\n", k.c_str());
             return 2;
@@ -137,7 +202,27 @@ int main(int argc, char** argv) {
         double regVal = 0.0;
         CHECK(psgd_initial_regval(ctx, &p, d, weights.data(), &regVal));   // :231-233
         bool converged = false, have_current = false;
-        for (int i = 1; !converged && i <= iterations; ++i) {              // :237
+        int first = 1;
+        const std::vector<double> fp = ckpt_fingerprint(p, data->n_rows, data->n_parts, d);
+        if (!checkpoint.empty()) {
+            LoopState st;
+            const int r = ckpt_load(checkpoint, fp, d, st);
+            if (r < 0) {
+                std::fprintf(stderr, "psgd_run: checkpoint %s was written by a run with other parameters "
+                                     "or data\n", checkpoint.c_str());
+                return 2;
+            }
+            if (r > 0) {
+                first = st.i;
+                regVal = st.regVal;
+                have_current = st.have_current != 0;
+                converged = st.converged != 0;
+                history = st.history;
+                weights = st.weights;
+                std::fprintf(stderr, "WARN resuming at iteration %d from checkpoint %s\n", first, checkpoint.c_str());
+            }
+        }
+        for (int i = first; !converged && i <= iterations; ++i) {          // :237
             p.iteration = i;
             double avgRegVal = 0.0, lossSum = 0.0;
             int64_t batchSize = 0;
@@ -155,6 +240,19 @@ int main(int argc, char** argv) {
             } else {                                                        // :295-297
                 std::fprintf(stderr, "WARN Iteration (%d/%d). The size of sampled batch is zero\n",
                              i, iterations);
+            }
+            if (!checkpoint.empty()) {
+                LoopState st;
+                st.i = i + 1;
+                st.regVal = regVal;
+                st.have_current = have_current;
+                st.converged = converged;
+                st.history = history;
+                st.weights = weights;
+                if (!ckpt_save(checkpoint, fp, st)) {
+                    std::fprintf(stderr, "psgd_run: cannot write checkpoint %s\n", checkpoint.c_str());
+                    return 1;
+                }
             }
         }
     }

@@ -76,3 +76,31 @@ def test_native_driver_matches_oracle(pkg, oracle, tmp_path, grad, upd, step, it
     assert_close(out["loss"], hr, what="loss")
     counts = np.array(out["chain_counts"], dtype=np.int64).reshape(-1, P)
     np.testing.assert_array_equal(counts, np.asarray(cr, dtype=np.int64).reshape(-1, P))
+
+
+@pytest.mark.gpu
+def test_native_driver_checkpoint_resume(tmp_path):
+    """--checkpoint FILE: a run stopped after 2 iterations and resumed to 6 prints the weights and
+    loss history of the uninterrupted 6-iteration run, bit for bit; a checkpoint of other
+    parameters is refused (exit 2)."""
+    if not has_gpu():
+        pytest.skip("no GPU")
+    need_bin()
+    f = tmp_path / "train.libsvm"
+    write_libsvm(f, 900, 50, seed=5)
+    base = [BIN, str(f), "--partitions", "3", "--gradient", "logistic", "--updater", "squared_l2",
+            "--step", "0.5", "--reg", "0.01", "--tol", "0"]
+    run = lambda *extra: subprocess.run(base + list(extra), capture_output=True, text=True, timeout=120)
+    full = run("--iterations", "6")
+    assert full.returncode == 0, full.stderr
+    ck = str(tmp_path / "loop.ck")
+    first = run("--iterations", "2", "--checkpoint", ck)
+    assert first.returncode == 0, first.stderr
+    res = run("--iterations", "6", "--checkpoint", ck)
+    assert res.returncode == 0 and "resuming at iteration 3" in res.stderr, res.stderr
+    a = json.loads(full.stdout.strip().splitlines()[-1])
+    b = json.loads(res.stdout.strip().splitlines()[-1])
+    assert a["weights"] == b["weights"] and a["loss"] == b["loss"] and len(b["loss"]) == 6
+    other = subprocess.run(base[:-1] + ["0.001", "--iterations", "6", "--checkpoint", ck],
+                           capture_output=True, text=True, timeout=120)
+    assert other.returncode == 2 and "other parameters" in other.stderr
