@@ -124,7 +124,9 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
     const int chain = blockIdx.x;
     const ChainDesc dsc = L.descs[chain];
     const int d = kp.d;
-    const int64_t n = dsc.n_rows;
+    // a chain's rows live in HBM at >= 1 KiB each (two row vectors on), so n < 2^31: the
+    // per-sample bookkeeping runs in 32-bit (one SALU op per step, v_cvt_f32/f64_i32 for iter)
+    const int32_t n = (int32_t)dsc.n_rows;
     const int MB = geom.meta_blocks;
 
     if (threadIdx.x == 0) {
@@ -172,7 +174,7 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
     double yb[2], sb[2];
     int meta_blk = 0;
     // the LDS reads of row t's slice and meta into buffer p (issued here, waited for at first use)
-    auto read_row = [&](auto pc, const char* src, int64_t t) __attribute__((always_inline)) {
+    auto read_row = [&](auto pc, const char* src, int32_t t) __attribute__((always_inline)) {
         constexpr int p = decltype(pc)::value;
 #pragma unroll
         for (int u = 0; u < NVH; ++u) {
@@ -198,12 +200,12 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
     // leaves the branch, so no LDS read waits at its join. false: the chain stopped.
     unsigned ready = 0;
     bool stop = false;
-    auto wait_rows = [&](int64_t rows) __attribute__((always_inline)) {
-        if (rows > (int64_t)ready) {
+    auto wait_rows = [&](int32_t rows) __attribute__((always_inline)) {
+        if (rows > (int32_t)ready) {
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             for (;;) {
                 ready = __hip_atomic_load(&hdr->ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (rows <= (int64_t)ready) break;
+                if (rows <= (int32_t)ready) break;
                 if (__hip_atomic_load(&hdr->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) { stop = true; break; }
                 if (__builtin_amdgcn_s_memrealtime() - t0 > kWatchdogTicks) {
                     __hip_atomic_fetch_or(L.watchdog, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -222,7 +224,7 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
     // in wave order. A stopped chain leaves collect with whatever it read (the host raises on the
     // watchdog word).
     constexpr uint64_t kMask = XW == 64 ? ~0ull : ((1ull << XW) - 1);
-    auto publish = [&](const T (&val)[KV], int64_t t) __attribute__((always_inline)) {
+    auto publish = [&](const T (&val)[KV], int32_t t) __attribute__((always_inline)) {
         const int k = lane / PC;
         T vk = val[0];
 #pragma unroll
@@ -237,7 +239,7 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
         if (lane < PC * KV)
             lds_write_u64(xw + (int)(t & 1) * XW + h * PC * KV + lane, ((uint64_t)(uint32_t)(t + 1) << 32) | piece);
     };
-    auto collect = [&](int64_t t, T (&sum)[KV]) __attribute__((always_inline)) {
+    auto collect = [&](int32_t t, T (&sum)[KV]) __attribute__((always_inline)) {
         const uint32_t tag = (uint32_t)(t + 1);
         const uint64_t* src = xw + (int)(t & 1) * XW + (lane < XW ? lane : 0);
         uint64_t v = lds_read_u64(src);
@@ -294,7 +296,7 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
     // CONV: this wave's ||w_old - w_new||^2, ||w_new||^2 of the last update (wave-reduced), the
     // sample at which the test of its predecessor broke the chain (n: no break)
     T pdsq = T(0), pnsq = T(0);
-    int64_t conv_at = n;
+    int32_t conv_at = n;
 
     // diagnostic builds (-DPSGD_STAMPS): cycles per phase of this wave's samples
     PSGD_STAMP(uint64_t st_dot = 0, st_x = 0, st_upd = 0; const uint64_t st_begin = __builtin_amdgcn_s_memtime();
@@ -304,7 +306,7 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
     // Sample t (row t in xb[p]): the partial dot and its wave reduction, publish; the reads of
     // row t + 1 go out before the poll so that their LDS latency overlaps the exchange's; then
     // the multiplier and this wave's updates. Straight-line: the only branches spin.
-    auto sample = [&](auto pc, int64_t t) __attribute__((always_inline)) {
+    auto sample = [&](auto pc, int32_t t) __attribute__((always_inline)) {
         constexpr int p = decltype(pc)::value;
         const T y = T(yb[p]);
         const T s = T(sb[p]);
@@ -451,7 +453,7 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
         wait_rows(1);
         read_row(std::integral_constant<int, 0>{}, ring, 0);
     }
-    int64_t t = 0;
+    int32_t t = 0;
     for (; t + 2 <= n && !stop && conv_at == n; t += 2) {
         sample(std::integral_constant<int, 0>{}, t);
         if (conv_at < n) break;
