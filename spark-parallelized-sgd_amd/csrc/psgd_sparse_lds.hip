@@ -171,7 +171,7 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
     T* W = reinterpret_cast<T*>(lds + kWoff);                    // head weights [K]
     uint16_t* tagpos = reinterpret_cast<uint16_t*>(W + K);       // tail features K .. d-1
     // dword index of val[0] of the slot holding row u
-    auto val_off = [](int64_t u) __attribute__((always_inline)) -> unsigned {
+    auto val_off = [](int32_t u) __attribute__((always_inline)) -> unsigned {
         return (unsigned)((kSlotOff + (int64_t)(u & (SR - 1)) * (int64_t)sizeof(LdsSlot<T>)) / 4) + LCAP;
     };
     const int lane = threadIdx.x & 63;
@@ -179,19 +179,21 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
     const int chain = blockIdx.x;
     const ChainDesc dsc = L.descs[chain];
     const int d = kp.d;
-    const int64_t n = dsc.n_rows;
-    const int64_t NT = tag_entries(d, K);
+    // row indices run in 32-bit: a chain's rows (>= 16 B each with the label) live in HBM, so
+    // n < 2^31; the CSR offsets stay 64-bit (the loader's row_ptr values)
+    const int32_t n = (int32_t)dsc.n_rows;
+    const int32_t NT = (int32_t)tag_entries(d, K);
     // The chain runs n_pad samples (a multiple of its unroll SK + 1) and reads up to row
     // n_pad + SK ahead: the loader and the tagger stage n_fill rows, rows past n null (no
     // entries, label and step 0), so no read in the chain needs a condition.
     constexpr int GS = SK + 1;
-    const int64_t n_pad = (n + GS - 1) / GS * GS;
-    const int64_t n_fill = (n_pad + SK + 1 + 7) / 8 * 8;
+    const int32_t n_pad = (n + GS - 1) / GS * GS;
+    const int32_t n_fill = (n_pad + SK + 1 + 7) / 8 * 8;
     // [d] (tail used) + [128] the loader's dummy sources + [1024] the chain's dummy targets (in
     // T: for doubles the chain's slice of L.wf32 is twice as long, launch_sparse_lds64_chains)
     T* V = reinterpret_cast<T*>(L.wf32 + (int64_t)chain * L.wstride);
 
-    for (int64_t i = threadIdx.x; i < NT; i += blockDim.x) tagpos[i] = 0xFFFF;
+    for (int32_t i = threadIdx.x; i < NT; i += blockDim.x) tagpos[i] = 0xFFFF;
     for (int i = threadIdx.x; i < K; i += blockDim.x) W[i] = T(as_global(L.w_in)[i]);
     if (threadIdx.x < 8) reinterpret_cast<unsigned*>(hdr)[threadIdx.x] = 0;
     if constexpr (F64 && TAIL) {
@@ -205,15 +207,15 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
     uint64_t st_wait = 0;                     // diagnostic (PSGD_STAMPS): cycles spent waiting
     const uint64_t st_begin = __builtin_amdgcn_s_memtime();
     // wait until *flag >= need (cached in `seen`); false when the chain stopped or the watchdog fired
-    auto wait_for = [&](unsigned& seen, const unsigned* flag, int64_t need, int code)
+    auto wait_for = [&](unsigned& seen, const unsigned* flag, int32_t need, int code)
         __attribute__((always_inline)) -> bool {
-        if ((int64_t)seen >= need) return true;
+        if ((int32_t)seen >= need) return true;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         const uint64_t c0 = __builtin_amdgcn_s_memtime();
         for (;;) {
             // relaxed: the flags and the data are LDS, which one wave writes in program order
             seen = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if ((int64_t)seen >= need) {
+            if ((int32_t)seen >= need) {
                 __atomic_signal_fence(__ATOMIC_SEQ_CST);
                 st_wait += __builtin_amdgcn_s_memtime() - c0;
                 return true;
@@ -227,7 +229,7 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
             __builtin_amdgcn_s_sleep(1);
         }
     };
-    auto publish = [&](unsigned* flag, int64_t v) __attribute__((always_inline)) {
+    auto publish = [&](unsigned* flag, int32_t v) __attribute__((always_inline)) {
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         __hip_atomic_store(flag, (unsigned)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
@@ -250,9 +252,9 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
         const gptr<int32_t> dummy_i = as_global((const int32_t*)(V + d + lane));   // valid, unused
         const gptr<S> dummy_s = as_global((const S*)(V + d + 2 * lane));
         struct Batch { int64_t rb, re; double y, s; };
-        auto load_batch = [&](int64_t g) __attribute__((always_inline)) -> Batch {
+        auto load_batch = [&](int32_t g) __attribute__((always_inline)) -> Batch {
             Batch bt{0, 0, 0.0, 0.0};
-            const int64_t ti = g + lane;
+            const int32_t ti = g + lane;
             if (ti < n) {
                 const int64_t r = RIDX ? (int64_t)RIDX[ti] : ti;
                 bt.rb = RP[r];
@@ -288,11 +290,11 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
         // rows u0 .. u0 + 7 (those < n_fill) into their slots, each once the chain is done with the
         // row its slot held (row u - SR, read by the chain up to row u - SR + SK), published row
         // by row: the chain at sample t waits for row t + SK + 1
-        auto stage_group = [&](int64_t u0, const Group& G) __attribute__((always_inline)) -> bool {
+        auto stage_group = [&](int32_t u0, const Group& G) __attribute__((always_inline)) -> bool {
             bool good = true;
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
-                const int64_t u = u0 + q;
+                const int32_t u = u0 + q;
                 if (good && u < n_fill) {
                     good = wait_for(done, &hdr->done, u - SR + SK + 1, 16);
                     LdsSlot<T>& sl = slots[u & (SR - 1)];
@@ -317,7 +319,7 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
         Batch cur = load_batch(0);
         Group GA, GB;
         load_group(cur, 0, GA);
-        for (int64_t g = 0; g < n_fill; g += 64) {
+        for (int32_t g = 0; g < n_fill; g += 64) {
             const Batch nxt = load_batch(g + 64);
             // meta of rows g .. g + 63: their ring positions held rows g - 128 .. g - 65
             if (!wait_for(done, &hdr->done, g - 64, 16)) break;
@@ -356,16 +358,16 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
         constexpr int TB = 4;
         unsigned loaded = 0;
         uint16_t* dtag = reinterpret_cast<uint16_t*>(&hdr->dtag);
-        const int64_t chunk = ((NT + kSweepRows - 1) / kSweepRows + 255) & ~int64_t(255);
+        const int32_t chunk = ((NT + kSweepRows - 1) / kSweepRows + 255) & ~int32_t(255);
         static_assert(8 % TB == 0, "n_fill is a multiple of TB");
-        for (int64_t u0 = 0; u0 < n_fill; u0 += TB) {
+        for (int32_t u0 = 0; u0 < n_fill; u0 += TB) {
             constexpr int nb = TB;
             if (!wait_for(loaded, &hdr->loaded, u0 + nb, 32)) break;
             int nnz[TB];
             int32_t ca[TB], cb[TB];
 #pragma unroll
             for (int q = 0; q < TB; ++q) {
-                const int64_t u = u0 + q;
+                const int32_t u = u0 + q;
                 const LdsSlot<T>& sl = slots[u & (SR - 1)];
                 nnz[q] = meta->nnz[u & (kMetaRing - 1)];
                 ca[q] = sl.col[lane];
@@ -389,11 +391,11 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
                 // one 4-tag word per lane and row: the TB reads share one LDS round trip
                 uint64_t sv[TB];
                 bool sok[TB];
-                int64_t si[TB];
+                int32_t si[TB];
 #pragma unroll
                 for (int q = 0; q < TB; ++q) {
-                    const int64_t lo = ((u0 + q) & (kSweepRows - 1)) * chunk;
-                    const int64_t hi = lo + chunk < NT ? lo + chunk : NT;
+                    const int32_t lo = ((u0 + q) & (kSweepRows - 1)) * chunk;
+                    const int32_t hi = lo + chunk < NT ? lo + chunk : NT;
                     si[q] = lo + 4 * lane;
                     sok[q] = si[q] < hi;
                     sv[q] = *reinterpret_cast<const uint64_t*>(tagpos + (sok[q] ? si[q] : 0));
@@ -404,9 +406,9 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
             } else {
 #pragma unroll
             for (int q = 0; q < TB; ++q) {
-                const int64_t lo = ((u0 + q) & (kSweepRows - 1)) * chunk;
-                const int64_t hi = lo + chunk < NT ? lo + chunk : NT;
-                for (int64_t i = lo + 4 * lane; i < hi; i += 256) {
+                const int32_t lo = ((u0 + q) & (kSweepRows - 1)) * chunk;
+                const int32_t hi = lo + chunk < NT ? lo + chunk : NT;
+                for (int32_t i = lo + 4 * lane; i < hi; i += 256) {
                     const uint64_t v = *reinterpret_cast<const uint64_t*>(tagpos + i);
                     *reinterpret_cast<uint64_t*>(tagpos + i) = sweep4(v);
                 }
@@ -415,7 +417,7 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
             unsigned va[TB], vb[TB];
 #pragma unroll
             for (int q = 0; q < TB; ++q) {
-                const int64_t u = u0 + q;
+                const int32_t u = u0 + q;
                 const bool ta_on = lane < nnz[q] && ca[q] >= K, tb_on = lane + 64 < nnz[q] && cb[q] >= K;
                 uint16_t* pa = ta_on ? tagpos + (ca[q] - K) : dtag;
                 uint16_t* pb = tb_on ? tagpos + (cb[q] - K) : dtag;
@@ -427,7 +429,7 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
             }
 #pragma unroll
             for (int q = 0; q < TB; ++q) {
-                const int64_t u = u0 + q;
+                const int32_t u = u0 + q;
                 auto rw_of = [&](int e, int32_t c, unsigned v) __attribute__((always_inline)) -> uint32_t {
                     const bool tail = c >= K;
                     const unsigned dl = ((unsigned)u - (v >> 8)) & 255;
@@ -475,17 +477,17 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
     T gr[GS][2];
     bool ok = true;
     // wait until rows < nl are loaded and rows < nt tagged (the spin path only)
-    auto need = [&](int64_t nl, int64_t nt) __attribute__((always_inline)) {
+    auto need = [&](int32_t nl, int32_t nt) __attribute__((always_inline)) {
         nl = nl < n_fill ? nl : n_fill;
         nt = nt < n_fill ? nt : n_fill;
-        if ((int64_t)loaded < nl || (int64_t)tagged < nt) {
+        if ((int32_t)loaded < nl || (int32_t)tagged < nt) {
             ok = ok && wait_for(loaded, &hdr->loaded, nl, 2);
             ok = ok && wait_for(tagged, &hdr->tagged, nt, 4);
         }
     };
     // the entries of row u a gather needs
     struct GCols { int32_t c0, c1; int nnz; };
-    auto gcols = [&](int64_t u) __attribute__((always_inline)) -> GCols {
+    auto gcols = [&](int32_t u) __attribute__((always_inline)) -> GCols {
         const LdsSlot<T>& sl = slots[u & (SR - 1)];
         const int nz = meta->nnz[u & (kMetaRing - 1)];
         return GCols{sl.col[lane], sl.col[lane + 64], nz};
@@ -502,7 +504,7 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
     };
     // the data of sample t
     struct Row { T x0, x1; uint32_t rw0, rw1; int32_t c0, c1; int nnz; T y, s; double s64; };
-    auto row_of = [&](int64_t t) __attribute__((always_inline)) -> Row {
+    auto row_of = [&](int32_t t) __attribute__((always_inline)) -> Row {
         const LdsSlot<T>& sl = slots[t & (SR - 1)];
         const int m = (int)(t & (kMetaRing - 1));
         return Row{sl.val[lane], sl.val[lane + 64], sl.rw[lane], sl.rw[lane + 64], sl.col[lane],
@@ -525,7 +527,7 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
         need(0, 1);
     }
     Row cur = row_of(0);
-    auto sample = [&](auto qc, int64_t t) __attribute__((always_inline)) {
+    auto sample = [&](auto qc, int32_t t) __attribute__((always_inline)) {
         constexpr int Q = decltype(qc)::value;           // t % GS
         constexpr int QN = (Q + SK) % GS;                 // (t + SK) % GS
         // the rows the reads below need (a branch to the spin only)
@@ -599,7 +601,7 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
         publish(&hdr->done, t + 1);
         cur = nxt;
     };
-    for (int64_t t = 0; ok && t < n_pad; t += GS)
+    for (int32_t t = 0; ok && t < n_pad; t += GS)
         static_for<GS>([&](auto qc) { sample(qc, t + decltype(qc)::value); });
     count = ok ? n : 0;
     __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
