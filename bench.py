@@ -45,7 +45,7 @@ SECONDARY_ROWS = {"c5": 20_000_000}
 # reference's own Double rows (8,200 B per sample)
 # (AdaGrad / Adam on the logistic c3 shard: the reference's Adam, r^iter in fix1 (UPD.scala:262),
 # turns NaN once the squared-gradient average r exceeds 1, which least squares at c2 reaches)
-DEFAULT_SECONDARY = ("c3:f64::f64,c3:f64,c3:f32,c2:f64,c1:f64,c4:f32,c4:f64,c5:f32,"
+DEFAULT_SECONDARY = ("c3:f64::f64,c3:f64,c3:f32,c2:f64,c1:f64,c4:f32,c4:f64,c4:f64::f64,c5:f32,c5:f64,"
                      "c3:f32:adagrad,c3:f32:adam,c3:f64:adagrad,c3:f64:adam")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
@@ -80,6 +80,8 @@ def pmc_traffic(workload, grad, variant, storage, rows, compute="f32", updater="
         prefix = f"psgd::chain_sparse_lds<{sname}, {tname}, {g}, {u},"
     elif variant >= 500:
         prefix = f"psgd::chain_block64<{sname}, {g}, {u}, {variant - 500},"
+    elif variant >= 420:
+        prefix = f"psgd::chain_sparse64<{sname}, {g}, {u}>"
     elif variant >= 410:
         prefix = f"psgd::chain_sparse_spec<{sname}, {g}, {u}"
     elif variant >= 400:
@@ -115,6 +117,9 @@ def kernel_name(variant):
         prec = "fp64" if (variant % 100) >= 20 else "fp32"
         return (f"chain_sparse_lds ({prec} CSR chain, weights LDS-resident [tail past ~160 KiB: L2-resident, "
                 f"gathered {8 if (variant % 20) >= 10 else 4} samples ahead with an LDS feature-tag correction])")
+    if 420 <= variant < 430:
+        return ("chain_sparse64 (fp64 CSR chain, weights as double vectors in HBM, alpha-scaled SquaredL2, "
+                "one gather round trip per sample)")
     if 410 <= variant < 420:
         return ("chain_sparse_spec (fp32 CSR chain, weights L2/MALL-resident, gathers 8 samples "
                 "ahead with an LDS feature-tag correction)")
@@ -144,6 +149,9 @@ def parse():
     ap.add_argument("--updater", default="", help="another SGDUpdater for the headline workload (experiments)")
     ap.add_argument("--storage", default="", choices=["", "f32", "f64"],
                     help="row storage dtype of the headline workload (default: the workload's own)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for --gpus > 1: nccl (RCCL over xGMI, one GPU per rank) or "
+                         "gloo (a CPU rehearsal of the multi-rank path; ranks may share one GPU)")
     ap.add_argument("--prewarm-s", type=float, default=1.0,
                     help="untimed epochs for this long before the warmup steps (GPU clock ramp)")
     return ap.parse_args()
@@ -215,9 +223,10 @@ def host_cpus():
     return n
 
 
-def cpu_baseline(grad, d, P, step, budget_s, seed=7, csr_nnz=0):
+def cpu_baseline(grad, d, P, step, budget_s, seed=7, csr_nnz=0, updater="simple", reg=0.0):
     """Time the CPU restatement of the reference (oracle/, one thread per partition, all host
-    cores) on a bounded sample of the same workload: the first m rows of every partition."""
+    cores) on a bounded sample of the same workload -- its gradient and SGDUpdater -- the first m
+    rows of every partition."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
@@ -250,7 +259,7 @@ def cpu_baseline(grad, d, P, step, budget_s, seed=7, csr_nnz=0):
     total, epochs = 0, 0
     t0 = time.perf_counter()
     while True:
-        w_out, _, _, cnt = O.run_chains(mat, offs, grad, "simple", step, 0.0, w, tol=0.0,
+        w_out, _, _, cnt = O.run_chains(mat, offs, grad, updater, step, reg, w, tol=0.0,
                                         n_threads=cores)
         total += int(cnt.sum())
         epochs += 1
@@ -261,16 +270,48 @@ def cpu_baseline(grad, d, P, step, budget_s, seed=7, csr_nnz=0):
     return {"value": total / dt, "unit": "samples/s", "cores": cores, "kind": "port",
             "host_cpus": host_cpus(), "nproc": os.cpu_count(),
             "sample": f"oracle/psgd_oracle.c (fp64 CPU restatement of ParallelizedSGD.scala:243-270 "
-                      f"incl. per-sample isConverged), {P} partitions x {m} "
+                      f"incl. per-sample isConverged; {grad}, {updater}), {P} partitions x {m} "
                       f"{'CSR (%d nnz) ' % csr_nnz if csr_nnz else ''}rows, d={d}, "
                       f"{epochs} epochs, {cores} threads, {dt:.1f} s"}
 
 
+def cpu_baseline_c1(budget_s, seed=42):
+    """BASELINE configs[0] on the CPU: logistic, dense 100k x 100 fp64, 4 partitions, one thread
+    per partition (Spark local[4]); the CPU restatement's whole epochs, repeated for budget_s."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    grad, n, d, P, step = WORKLOADS["c1"][:5]
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((n, d))
+    w_star = rng.standard_normal(d) / np.sqrt(d)
+    y = ((X @ w_star + rng.logistic(size=n)) > 0).astype(float)
+    mat = O.Matrix(y, X)
+    offs = [p * n // P for p in range(P + 1)]
+    w = np.zeros(d)
+    total, epochs = 0, 0
+    t0 = time.perf_counter()
+    while True:
+        w_out, _, _, cnt = O.run_chains(mat, offs, grad, "simple", step, 0.0, w, tol=0.0, n_threads=P)
+        total += int(cnt.sum())
+        epochs += 1
+        w = w_out.mean(axis=0)
+        dt = time.perf_counter() - t0
+        if dt >= budget_s:
+            break
+    return {"value": total / dt, "unit": "samples/s", "cores": P, "kind": "port",
+            "sample": f"oracle/psgd_oracle.c, the whole c1 epoch ({n} x {d} fp64, {P} partitions, "
+                      f"{P} threads = local[{P}]), {epochs} epochs, {dt:.1f} s"}
+
+
 def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, rows, fraction,
-                 steps, warmup, prewarm_s, features=0, chains=0, updater="", storage=""):
+                 steps, warmup, prewarm_s, features=0, chains=0, updater="", storage="", backend="nccl"):
     """One workload: synthetic shard in HBM, prewarm, W warmup steps, K timed steps (barrier +
     synchronize on both sides, max over ranks). Returns the measurement as a dict."""
     import numpy as np
+    # the ranks' scalar agreements (prewarm epoch count, elapsed time): device tensors over RCCL,
+    # host tensors over gloo
+    red_dev = dev if backend == "nccl" else torch.device("cpu")
     grad, n, d, P, step, sdt, cfg_name = WORKLOADS[workload]
     if storage and storage != sdt:
         sdt = storage
@@ -349,7 +390,7 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
         per_epoch = (time.perf_counter() - t_pw) / 2
         want = max(2, min(5000, int(prewarm_s / max(per_epoch, 1e-6))))
         if world > 1:
-            t = torch.tensor([want], dtype=torch.int64, device=dev)
+            t = torch.tensor([want], dtype=torch.int64, device=red_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             want = int(t.item())
         while prewarm_epochs < want:
@@ -377,7 +418,7 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     # `cnt` is the whole job's sample count of the step (the fold sums counts over all ranks)
@@ -392,14 +433,23 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
     avg_epoch_s = sum(epoch_ms) / len(epoch_ms) / 1e3
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
     es = 4 if sdt == "f32" else 8
-    if csr:  # values + int32 columns + int64 row pointer + f64 label (weights: L2/MALL-resident)
-        bytes_per_sample = CSR_NNZ[workload] * (es + 4) + 8 + 8
+    variant = engine.ctx.last_kernel()
+    offchip = None
+    if csr:
+        # the row stream -- values + int32 columns + int64 row pointer + f64 label --
+        # plus, when the chain's weights are not on chip, their gather and scatter (2 nnz
+        # sizeof(T)). chain_sparse_lds keeps them in LDS (its tail in L2): the row stream is its
+        # figure; chain_sparse / chain_sparse64 / chain_general keep them in HBM: the sum is theirs.
+        # The line carries both.
+        rowstream = CSR_NNZ[workload] * (es + 4) + 8 + 8
+        offchip = rowstream + 2 * CSR_NNZ[workload] * (4 if compute == "f32" else 8)
+        weights_on_chip = 600 <= variant < 700
+        bytes_per_sample = rowstream if weights_on_chip else offchip
     else:
         bytes_per_sample = (d + 1) * es  # row + label (weights are on chip)
     local_samples = n if fraction >= 1.0 else samples_per_step / world
     # one chain-kernel launch processes every (sampled) row of this GPU's partitions
     achieved = local_samples * bytes_per_sample / avg_kernel_s / 1e9
-    variant = engine.ctx.last_kernel()
     upd_name = updater or ("squared_l2" if reg > 0 else "simple")
     traffic, traffic_src = pmc_traffic(workload, grad, variant, sdt, n, compute, upd_name)
     note = None
@@ -413,18 +463,26 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
                    "chains_per_gpu": P, "storage": sdt, "gradient": grad,
                    "updater": updater or ("squared_l2" if reg > 0 else "simple"), "reg_param": reg,
                    "step_size": step, "convergence_tol": 0.0, "mini_batch_fraction": fraction,
-                   "parallelism": f"dp{world} (chains sharded, RCCL all-gather + fold per epoch)"},
+                   "parallelism": f"dp{world}" + (" (chains sharded, RCCL all-gather + fold per epoch)"
+                                                   if backend == "nccl" else
+                                                   " (chains sharded, gloo all-gather + fold per epoch: a rehearsal)")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src,
                      "kernel": kernel_name(variant),
                      "bytes_per_launch": local_samples * bytes_per_sample,
-                     "bytes_per_sample": bytes_per_sample, "avg_kernel_ms": avg_kernel_s * 1e3,
+                     "bytes_per_sample": bytes_per_sample,
+                     **({"bytes_per_sample_rowstream": rowstream,
+                         "frac_rowstream": local_samples * rowstream / avg_kernel_s / 1e9 / HBM_PEAK_GBS,
+                         "bytes_per_sample_weights_offchip": offchip,
+                         "frac_weights_offchip": local_samples * offchip / avg_kernel_s / 1e9 / HBM_PEAK_GBS}
+                        if csr else {}),
+                     "avg_kernel_ms": avg_kernel_s * 1e3,
                      "avg_epoch_ms": avg_epoch_s * 1e3,
                      "timing": "HIP events recorded around each chain-kernel launch on its stream"},
         "prewarm": {"seconds": prewarm_s, "epochs": prewarm_epochs,
                     "note": "untimed epochs before the warmup steps (GPU clock ramp); their model is discarded"},
-        "_meta": (grad, d, P, step, csr),
+        "_meta": (grad, d, P, step, csr, upd_name, reg),
     }
     del engine, data, parts, all_parts
     return res
@@ -455,16 +513,22 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.backend == "gloo":
+        # a rehearsal of the multi-rank path on fewer GPUs than ranks (ranks share devices)
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
     res = run_workload(torch, dist, pkg, dev, rank, world, local, args.workload, args.compute,
                        args.rows, args.fraction, args.steps, args.warmup, args.prewarm_s, args.features,
-                       args.chains, args.updater, args.storage)
-    grad, d, P, step, csr = res.pop("_meta")
+                       args.chains, args.updater, args.storage, args.backend)
+    grad, d, P, step, csr, upd_name, reg = res.pop("_meta")
     res.pop("loss")
     out = {
         "metric": "training samples/sec (whole node) + achieved HBM GB/s, logistic SGD 1/2/4/8 GPUs",
@@ -476,7 +540,11 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(grad, d, P, step, args.cpu_seconds,
-                                           csr_nnz=CSR_NNZ[args.workload] if csr else 0)
+                                           csr_nnz=CSR_NNZ[args.workload] if csr else 0,
+                                           updater=upd_name, reg=reg)
+        # BASELINE configs[0], the reference's own CPU case (Spark local[4]): its CPU rate in the
+        # same run, beside the c1 GPU secondary line
+        out["cpu_baseline_c1"] = cpu_baseline_c1(min(args.cpu_seconds, 4.0))
     # Secondary lines (one GPU only): the other BASELINE configs' per-GPU workloads under the
     # same clock, each with its own roofline (VERDICT r01 "let the driver observe" them).
     secondary = [s for s in args.secondary.split(",") if s] if world == 1 else []

@@ -898,6 +898,15 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
     const int state_vectors = !need_state ? 0 : (mn || layout == psgd::kCsr) ? 3 : 2;
     rc = prepare(ctx, dw, state_vectors, st);
     if (rc) return rc;
+    // from here on work may be queued on `st` (descriptor upload, sampling, a chain kernel that
+    // launched before a later launch failed): every return records the scratch event, so that
+    // psgd_clear_partitions (which waits on it instead of the whole device) cannot free buffers
+    // under a kernel that is still running
+    struct ScratchGuard {
+        psgd_ctx* ctx;
+        hipStream_t st;
+        ~ScratchGuard() { (void)scratch_release(ctx, st); }
+    } scratch_guard{ctx, st};
     int64_t n_max = 0, max_ld = 0, min_ld = INT64_MAX, max_nnz = 0;
     for (auto& kv : ctx->parts) {
         n_max = std::max(n_max, kv.second.n_rows);
@@ -912,6 +921,9 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
     // f <= 0 gives every partition empty, f >= 1 every row, else a Bernoulli batch per partition
     const bool sample_empty = params->mini_batch_fraction <= 0.0;
     const bool sampled = !sample_empty && params->mini_batch_fraction < 1.0;
+    // the sampled batch's row indices are int32 (ChainDesc::rows)
+    if (sampled && n_max > (int64_t)INT32_MAX)
+        return fail(PSGD_EUNSUPPORTED, "miniBatchFraction < 1 on a partition of more than 2^31 - 1 rows");
     rc = ensure_steps(ctx, params->step_size, n_max, st);
     if (rc) return rc;
 
@@ -983,11 +995,15 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         L.wnsq0 = ctx->wnsq0.as<double>();
     }
     if (layout == psgd::kCsr && params->compute_dtype == PSGD_F64 && !mn &&
-        psgd::sparse_lds64_applies(d, max_nnz, params->updater, conv, true)) {
-        // the fp64 CSR kernel's per-chain f64 vectors (d + 1152 doubles, in L.wf32's memory)
+        (psgd::sparse_lds64_applies(d, max_nnz, params->updater, conv, true, n_max) ||
+         psgd::sparse64_path_applies(layout, 0, params->updater, conv, true))) {
+        // the fp64 CSR kernels' per-chain f64 vectors (d + 1152 doubles, in L.wf32's memory) and
+        // chain_sparse64's alphas
         L.wstride = 2 * (((int64_t)d + 128 + 1024 + 63) / 64 * 64);
         HIP_TRY(ctx->wf32.ensure((size_t)P * (size_t)L.wstride * sizeof(float)));
+        HIP_TRY(ctx->walpha.ensure((size_t)P * sizeof(double)));
         L.wf32 = ctx->wf32.as<float>();
+        L.walpha = ctx->walpha.as<double>();
     }
     if (params->gradient == PSGD_GRADIENT_LOGISTIC && params->compute_dtype == PSGD_F32 &&
         layout == psgd::kDense) {
@@ -1013,10 +1029,11 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
     kp.d = d;
     kp.n_chains = P;
     kp.nc = mn ? params->num_classes - 1 : 0;
+    kp.n_max = n_max;
     kp.alpha_ok = params->updater != PSGD_UPDATER_SQUARED_L2 ||
                   alpha_in_range(ctx, params->step_size, params->reg_param, n_max);
 
-    bool from_wf32 = false;   // the launch left the chains' weights in L.wf32 (fp32 CSR kernels)
+    int weights_in = psgd::kWeightsOut;   // where the launch left the chains' weights
     if (sample_empty) {
         // RDD.sample with fraction 0: every partition is empty -> (w_in, 0, 0, 0) per chain.
         for (int p = 0; p < P; ++p)
@@ -1036,7 +1053,7 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
                                     params->compute_dtype == PSGD_F32 ? 1 : 0, params->gradient,
                                     params->updater, conv, min_ld, max_ld,
                                     lds_spread_bytes(ctx, (size_t)P), st, &ctx->last_variant, max_nnz,
-                                    &from_wf32);
+                                    &weights_in);
         HIP_TRY(hipEventRecord(ctx->ev_end, st));
         ctx->ev_recorded = (e == 0);
         if (L.stamps) {   // PSGD_STAMPS=1: per-chain cycle counters of the CSR fp32 kernels (stderr)
@@ -1068,16 +1085,19 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         if (e) return fail(PSGD_EDEVICE, std::string("chain kernel launch failed: ") +
                                              hipGetErrorString((hipError_t)e));
     }
-    // the fp32 CSR kernels leave each chain's weights in L.wf32 (w = alpha v)
-    int e = from_wf32
+    // the CSR kernels of L.wf32 leave each chain's weights there (w = alpha v, floats or doubles)
+    int e = weights_in == psgd::kWeightsF32
                 ? psgd::launch_fold_f32(L.wf32, L.wstride, L.walpha, L.rv, L.loss, L.cnt_d, P, dw, d_partial,
                                         L.watchdog, st)
+            : weights_in == psgd::kWeightsF64
+                ? psgd::launch_fold_f64(reinterpret_cast<const double*>(L.wf32), L.wstride / 2, L.walpha, L.rv,
+                                        L.loss, L.cnt_d, P, dw, d_partial, L.watchdog, st)
                 : psgd::launch_fold(L.w_out, dw, L.rv, L.loss, L.cnt_d, 1, P, dw, d_partial, L.watchdog, st);
     if (e) return fail(PSGD_EDEVICE, "fold kernel launch failed");
     if (d_chain_counts)
         HIP_TRY(hipMemcpyAsync(d_chain_counts, L.cnt, (size_t)P * sizeof(int64_t),
                                hipMemcpyDeviceToDevice, st));
-    return scratch_release(ctx, st);
+    return PSGD_OK;   // scratch_guard records the scratch event
 }
 
 int32_t psgd_run_epoch(psgd_ctx* ctx, const psgd_params* params, const double* w_in,

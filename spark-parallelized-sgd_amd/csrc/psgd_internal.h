@@ -30,6 +30,9 @@ struct KParams {
     // prefix product of (1 - s_j lambda), j <= the longest chain, is finite, non-zero and within
     // [2^-400, 2^400] (set by the host; chain_sparse_lds in fp64 runs only then)
     int32_t alpha_ok = 0;
+    // the longest chain of the epoch (before sampling): kernels that count rows in 32 bits apply
+    // only while it is <= INT32_MAX
+    int64_t n_max = 0;
 };
 
 // LogisticGradient(numClasses = K): at most this many weight blocks (K - 1), the chain keeps
@@ -37,6 +40,7 @@ struct KParams {
 constexpr int kMultinomialMaxBlocks = 4096;
 
 enum Layout { kDense = 0, kCsr = 1 };
+enum WeightsIn { kWeightsOut = 0, kWeightsF32 = 1, kWeightsF64 = 2 };
 
 // Everything a chain launch needs (device pointers).
 struct ChainLaunch {
@@ -75,14 +79,15 @@ struct ChainLaunch {
 // storage: 0 = f64, 1 = f32; compute: 0 = f64, 1 = f32.
 // Kernel variants (*kernel_variant, psgd_ctx_last_kernel): 100 + NV chain_dense, 200 + LAYOUT
 // chain_general, 300 + NV chain_block, 400 + storage chain_sparse, 410 + storage chain_sparse_spec,
-// 500 + LAYOUT chain_multinomial, 600 + 10 (SK 8) + 20 (fp64) + storage chain_sparse_lds,
+// 420 + storage chain_sparse64, 500 + LAYOUT chain_multinomial, 600 + 10 (SK 8) + 20 (fp64) + storage chain_sparse_lds,
 // 700 + 10 (H - 1) + NV chain_block64, 800 + 10 H + NV chain_split.
-// *weights_in_wf32 (nullable): the launch left each chain's weights in L.wf32 (w = walpha v, the
-// fp32 CSR kernels), to be folded by launch_fold_f32; else they are in L.w_out.
+// *weights_in (nullable): where the launch left each chain's weights -- kWeightsOut: L.w_out
+// (launch_fold); kWeightsF32: L.wf32 as floats, w = walpha v (the fp32 CSR kernels,
+// launch_fold_f32); kWeightsF64: L.wf32 as doubles, w = walpha v (chain_sparse64, launch_fold_f64).
 int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int storage, int compute,
                   int gradient, int updater, bool check_conv, int64_t min_ld, int64_t max_ld,
                   int lds_spread, hipStream_t stream, int* kernel_variant, int64_t max_nnz = 0,
-                  bool* weights_in_wf32 = nullptr);
+                  int* weights_in = nullptr);
 // The blocked fp32 kernel (psgd_block.hip): dense rows, Simple/SquaredL2, no per-sample
 // convergence test. launch_block_chains returns -3 when it does not apply.
 bool block_path_applies(int layout, int compute, int updater, bool check_conv, int storage,
@@ -114,16 +119,27 @@ int launch_steps(double step, int64_t n, double* steps, hipStream_t stream);
 bool sparse_path_applies(int layout, int compute, int updater, bool check_conv);
 int launch_sparse_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
                          int updater, int64_t max_nnz, hipStream_t stream, int* kernel_variant);
+// The fp64 CSR chain with HBM-resident weights (psgd_sparse.hip, chain_sparse64): Simple, and
+// SquaredL2 when kp.alpha_ok; the chain's double vector lives in its slice of L.wf32 (>= 2 (d +
+// 1152) floats), its alpha in L.walpha; weights end there (w = walpha v, launch_fold_f64).
+bool sparse64_path_applies(int layout, int compute, int updater, bool check_conv, bool alpha_ok);
+int launch_sparse64_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
+                           int updater, hipStream_t stream, int* kernel_variant);
+// The combiner over chain_sparse64's vectors: w_p = walpha[p] * v_p[i] (v_p doubles).
+int launch_fold_f64(const double* wv, int64_t wstride_d, const double* walpha, const double* rv,
+                    const double* loss, const double* cnt, int n, int d, double* out,
+                    const int* watchdog, hipStream_t stream);
 // The fp32 CSR kernel with LDS-resident weights (psgd_sparse_lds.hip): rows of <= 128 non-zeros,
 // features [0, K) in LDS and [K, d) in L.wf32; -3 when it does not apply.
-bool sparse_lds_applies(int64_t d, int64_t max_nnz);
+bool sparse_lds_applies(int64_t d, int64_t max_nnz, int64_t n_max);
 int64_t sparse_lds_head(int64_t d);
 int launch_sparse_lds_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
                              int updater, int64_t max_nnz, hipStream_t stream, int* kernel_variant);
 // The same kernel in fp64 compute (the parity mode's CSR throughput kernel): Simple, and
 // SquaredL2 when kp.alpha_ok; the chain's f64 vector lives in its slice of L.wf32, which must be
 // >= 2 (d + 1152) floats; weights end in L.w_out. -3 when it does not apply.
-bool sparse_lds64_applies(int64_t d, int64_t max_nnz, int updater, bool check_conv, bool alpha_ok);
+bool sparse_lds64_applies(int64_t d, int64_t max_nnz, int updater, bool check_conv, bool alpha_ok,
+                          int64_t n_max);
 int launch_sparse_lds64_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
                                int updater, int64_t max_nnz, hipStream_t stream, int* kernel_variant);
 // Longest row of a device-resident CSR partition (synchronises `st`).

@@ -20,6 +20,8 @@
 // norms are reassociated (wave tree instead of the F2J left fold), so fp64 mode agrees with the
 // reference to rounding, not bitwise.
 #include "psgd_device.h"
+
+#include <string.h>
 #include "psgd_split.h"
 
 #include <stdlib.h>
@@ -237,7 +239,7 @@ __global__ __launch_bounds__(128) void chain_dense(ChainLaunch L, KParams kp, Ri
                     nw.y = old.y + a * (g.y * __builtin_amdgcn_rsqf(acc2.y + T(1)));
                 } else {
                     // g / pow(accum + 1.0, 0.5) (UPD.scala:209) as g * rsqrt(accum + 1): v_rsq_f64
-                    // and two Newton steps (within ~2 ulp; the library sqrt + division were
+                    // and one Newton step (4.3e-15 relative, tools/newton_check; the library sqrt + division were
                     // ~20 dependent f64 operations per coordinate and sample)
                     nw.x = old.x + a * (g.x * rsqrt_newton(acc2.x + T(1)));
                     nw.y = old.y + a * (g.y * rsqrt_newton(acc2.y + T(1)));
@@ -669,7 +671,10 @@ __global__ void fold_kernel(const double* __restrict__ w, int64_t w_stride,
 // The same combiner over the fp32 CSR chains' weights, w_p = walpha[p] * double(v_p[i]) -- the
 // value those chains once wrote to w_out, so the fold's arithmetic is unchanged; reading the
 // fp32 vectors directly saves the O(P d) f64 write and re-read (C5: 2^22 features x 1024 chains).
-__global__ void fold_f32_kernel(const float* __restrict__ v, int64_t v_stride,
+// (V = double: chain_sparse64's vectors, the same combiner with w_p = walpha[p] * v_p[i] -- the
+// value chain_general's W[i] = alpha * W[i] writes at the chain's end.)
+template <typename V>
+__global__ void fold_scaled_kernel(const V* __restrict__ v, int64_t v_stride,
                                 const double* __restrict__ alpha, const double* __restrict__ rv,
                                 const double* __restrict__ loss, const double* __restrict__ cnt,
                                 int n, int d, double* __restrict__ out, const int* __restrict__ watchdog) {
@@ -704,7 +709,18 @@ int launch_fold_f32(const float* wf32, int64_t wstride, const double* walpha, co
     if (n <= 0) return -1;
     const int threads = 256;
     const int blocks = (d + 1 + threads - 1) / threads;
-    hipLaunchKernelGGL(fold_f32_kernel, dim3(blocks), dim3(threads), 0, stream, wf32, wstride, walpha,
+    hipLaunchKernelGGL(fold_scaled_kernel<float>, dim3(blocks), dim3(threads), 0, stream, wf32, wstride, walpha,
+                       rv, loss, cnt, n, d, out, watchdog);
+    return (int)hipGetLastError();
+}
+
+int launch_fold_f64(const double* wv, int64_t wstride_d, const double* walpha, const double* rv,
+                    const double* loss, const double* cnt, int n, int d, double* out,
+                    const int* watchdog, hipStream_t stream) {
+    if (n <= 0) return -1;
+    const int threads = 256;
+    const int blocks = (d + 1 + threads - 1) / threads;
+    hipLaunchKernelGGL(fold_scaled_kernel<double>, dim3(blocks), dim3(threads), 0, stream, wv, wstride_d, walpha,
                        rv, loss, cnt, n, d, out, watchdog);
     return (int)hipGetLastError();
 }
@@ -899,8 +915,8 @@ static int dispatch_grad(const ChainLaunch& L, const KParams& kp, int layout, in
 int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int storage, int compute,
                   int gradient, int updater, bool check_conv, int64_t min_ld, int64_t max_ld,
                   int lds_spread, hipStream_t stream, int* kernel_variant, int64_t max_nnz,
-                  bool* weights_in_wf32) {
-    if (weights_in_wf32) *weights_in_wf32 = false;
+                  int* weights_in) {
+    if (weights_in) *weights_in = kWeightsOut;
     if (kp.n_chains <= 0) return 0;
     if (kp.nc > 0)   // LogisticGradient(numClasses > 2)
         return launch_multinomial_chains(L, kp, layout, storage, updater, check_conv, stream, kernel_variant);
@@ -916,12 +932,22 @@ int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int stora
         return launch_block_chains(L, kp, storage, gradient, updater, min_ld, max_ld, lds_spread,
                                    stream, kernel_variant);
     if (!per_sample && sparse_path_applies(layout, compute, updater, check_conv)) {
-        if (weights_in_wf32) *weights_in_wf32 = true;
+        if (weights_in) *weights_in = kWeightsF32;
         return launch_sparse_chains(L, kp, storage, gradient, updater, max_nnz, stream, kernel_variant);
     }
-    if (!per_sample && layout == kCsr && compute == 0 &&
-        sparse_lds64_applies(kp.d, max_nnz, updater, check_conv, kp.alpha_ok != 0) && L.wf32)
+    // PSGD_SPARSE_KERNEL=hbm64 keeps fp64 CSR epochs off the LDS kernel (tests, A/B measurements;
+    // read at every launch)
+    const char* force = getenv("PSGD_SPARSE_KERNEL");
+    const bool hbm64 = force && strcmp(force, "hbm64") == 0;
+    if (!per_sample && !hbm64 && layout == kCsr && compute == 0 &&
+        sparse_lds64_applies(kp.d, max_nnz, updater, check_conv, kp.alpha_ok != 0, kp.n_max) && L.wf32)
         return launch_sparse_lds64_chains(L, kp, storage, gradient, updater, max_nnz, stream, kernel_variant);
+    // fp64 CSR beyond the LDS kernel's d (C5): the chain's weights as a double vector in HBM
+    if (!per_sample && sparse64_path_applies(layout, compute, updater, check_conv, kp.alpha_ok != 0) && L.wf32 &&
+        L.walpha) {
+        if (weights_in) *weights_in = kWeightsF64;
+        return launch_sparse64_chains(L, kp, storage, gradient, updater, stream, kernel_variant);
+    }
     if (!per_sample && split_path_applies(layout, updater, check_conv, storage, max_ld)) {
         const int e = launch_split_chains(L, kp, storage, compute, gradient, updater, min_ld, max_ld,
                                           lds_spread, stream, kernel_variant);

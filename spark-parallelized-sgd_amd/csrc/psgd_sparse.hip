@@ -140,6 +140,145 @@ __global__ __launch_bounds__(64) void chain_sparse(ChainLaunch L, KParams kp) {
 }
 
 // ------------------------------------------------------------------------------------------
+// chain_sparse64: the same walk in fp64 compute -- the parity mode's CSR chain for models whose
+// weights cannot live on chip (C5: 2^22 features), i.e. the reference's own arithmetic
+// (ParallelizedSGD.scala:253-268 on Double, SGDUpdater.scala:86-98 / :163-181).
+//   * the chain's weights are a double vector in HBM (its slice of L.wf32, 2 (d + 1152) floats;
+//     34 GB for C5's 1,024 chains), = w_in at the start (w64_init_kernel);
+//   * per sample: gathers of the row's weights (global_load_dwordx2 sc1, after this wave's earlier
+//     stores in L2), dot = per-lane fma over entries l, l + 64 and the wave tree (chain_general's
+//     order), Gradient.compute in Double (gradient_scalar<GRAD, double>), and the row's stores
+//     w_j + (-s) (mult x_j) (global_store_dwordx2); rows with mult = 0 (Hinge inside the margin)
+//     store nothing -- the reference's update adds a zero there;
+//   * SquaredL2 in the alpha-scaled form w = alpha v of chain_general (alpha *= 1 - s lambda, then
+//     v_j += ((-s)(mult x_j)) / alpha), valid without renormalisation only while every prefix
+//     product of the epoch stays in [2^-400, 2^400]: the host checks that (kp.alpha_ok) and runs
+//     chain_general otherwise;
+//   * regVal = 0.5 lambda ||alpha v||^2 after the last sample by one O(d) pass in chain_general's
+//     lane order; the fold reads w = alpha v straight from the vectors (fold_f64_kernel).
+// Everything but the dot's wave tree is chain_general's arithmetic operator for operator.
+// ------------------------------------------------------------------------------------------
+template <typename S, int GRAD, int UPD>
+__global__ __launch_bounds__(64) void chain_sparse64(ChainLaunch L, KParams kp) {
+    constexpr bool L2 = UPD == U_SQUARED_L2;
+    const int lane = threadIdx.x;
+    const int chain = blockIdx.x;
+    const ChainDesc dsc = L.descs[chain];
+    const int64_t n = dsc.n_rows;
+    const int d = kp.d;
+    const gptr<S> X = as_global(reinterpret_cast<const S*>(dsc.x));
+    const gptr<int32_t> COL = as_global(dsc.col);
+    const gptr<int64_t> RP = as_global(dsc.row_ptr);
+    const gptr<double> Y = as_global(dsc.y);
+    const gptr<double> STEPS = as_global(L.steps);
+    const gptr<int32_t> RIDX = dsc.rows ? as_global(dsc.rows) : nullptr;   // sampled epoch
+    double* V = reinterpret_cast<double*>(L.wf32 + (int64_t)chain * L.wstride);   // = w_in
+    const gmut<double> VW = as_global_mut(V);
+    // gathers: relaxed agent-scope loads (global_load_dwordx2 ... sc1, served by L2 after this
+    // wave's earlier stores to the same lines, as in chain_sparse); the compiler counts them
+    auto gather = [&](int32_t j) __attribute__((always_inline)) -> double {
+        return __hip_atomic_load(&V[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+
+    double alpha = 1.0;      // SquaredL2: w = alpha * v
+    double loss_sum = 0.0;
+    int64_t count = 0;
+
+    // software pipeline as chain_sparse: row t+1's entries, label and step and row t+2's range
+    // load under row t's gather
+    auto range_of = [&](int64_t t, int64_t& b, int64_t& e) __attribute__((always_inline)) {
+        if (t < n) {
+            const int64_t r = RIDX ? (int64_t)RIDX[t] : t;
+            b = RP[r];
+            e = RP[r + 1];
+        } else {
+            b = e = 0;
+        }
+    };
+    auto entries_of = [&](int64_t t, int64_t b, int64_t e, double& yy, double& ss, int32_t& ca,
+                          int32_t& cb, double& xa, double& xb) __attribute__((always_inline)) {
+        yy = t < n ? Y[t] : 0.0;
+        ss = t < n ? STEPS[t] : 0.0;
+        const int64_t ka = b + lane, kc = b + 64 + lane;
+        ca = ka < e ? COL[ka] : 0;
+        xa = ka < e ? double(X[ka]) : 0.0;
+        cb = kc < e ? COL[kc] : 0;
+        xb = kc < e ? double(X[kc]) : 0.0;
+    };
+    int64_t kb = 0, ke = 0, kb1 = 0, ke1 = 0;
+    double y = 0.0, s = 0.0;
+    int32_t c0 = 0, c1 = 0;
+    double x0 = 0.0, x1 = 0.0;
+    range_of(0, kb, ke);
+    range_of(1, kb1, ke1);
+    entries_of(0, kb, ke, y, s, c0, c1, x0, x1);
+
+    for (int64_t t = 0; t < n; ++t) {
+        const int64_t nnz = ke - kb;
+        const bool a0 = lane < nnz, a1 = lane + 64 < nnz;
+        const double w0 = a0 ? gather(c0) : 0.0;
+        const double w1 = a1 ? gather(c1) : 0.0;
+        double ny = 0.0, ns = 0.0;
+        int32_t n0 = 0, n1 = 0;
+        double nx0 = 0.0, nx1 = 0.0;
+        entries_of(t + 1, kb1, ke1, ny, ns, n0, n1, nx0, nx1);
+        int64_t kb2, ke2;
+        range_of(t + 2, kb2, ke2);
+
+        // dot(x, v): chain_general's per-lane fma order over entries lane, lane + 64, lane + 128, ...
+        double acc = m_fma(x0, w0, 0.0);
+        acc = m_fma(x1, w1, acc);
+        for (int64_t k = kb + 128 + lane; k < ke; k += 64) acc = m_fma(double(X[k]), gather(COL[k]), acc);
+        double z = wave_sum(acc);
+        if constexpr (L2) z = alpha * z;      // dot(x, w) with w = alpha v
+        double mult;
+        loss_sum += gradient_scalar<GRAD, double>(z, y, mult);
+        count += 1;
+        const double a = -s;
+        if constexpr (L2) alpha = alpha * (1.0 - s * kp.reg);
+        if (mult != 0.0) {
+            // v_j + (a * (mult * x_j)) [/ alpha] at the row's indices
+            double u0 = a * (mult * x0), u1 = a * (mult * x1);
+            if constexpr (L2) { u0 = u0 / alpha; u1 = u1 / alpha; }
+            if (a0) VW[c0] = w0 + u0;
+            if (a1) VW[c1] = w1 + u1;
+            for (int64_t k = kb + 128 + lane; k < ke; k += 64) {
+                const int32_t j = COL[k];
+                double u = a * (mult * double(X[k]));
+                if constexpr (L2) u = u / alpha;
+                VW[j] = gather(j) + u;
+            }
+        }
+        kb = kb1; ke = ke1; kb1 = kb2; ke1 = ke2;
+        y = ny; s = ns; c0 = n0; c1 = n1; x0 = nx0; x1 = nx1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    double rv = 0.0;
+    if constexpr (L2) {
+        // regVal = 0.5 lambda ||w||^2 of the last update (UPD.scala:176-180), w_i = alpha v_i, in
+        // chain_general's lane order (its W[i] = alpha * W[i]; acc += W[i] * W[i])
+        double nsq = 0.0;
+#pragma unroll 8
+        for (int i = lane; i < d; i += 64) {
+            const double wi = alpha * gather(i);
+            nsq += wi * wi;
+        }
+        nsq = wave_sum(nsq);
+        if (count > 0) {
+            const double nrm = sqrt(nsq);
+            rv = 0.5 * kp.reg * nrm * nrm;
+        }
+    }
+    if (lane == 0) {
+        L.walpha[chain] = alpha;
+        L.rv[chain] = rv;
+        L.loss[chain] = loss_sum;
+        L.cnt[chain] = count;
+        L.cnt_d[chain] = double(count);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // chain_sparse_spec: the same chain with the gathers issued SK samples ahead (rows of <= 128
 // non-zeros).
 //
@@ -589,6 +728,67 @@ static int sparse_epoch_init(const ChainLaunch& L, const KParams& kp, int update
     if (updater == U_SQUARED_L2)
         hipLaunchKernelGGL(wnsq0_kernel, dim3(1), dim3(1024), 0, st, L.w_in, kp.d, L.wnsq0);
     return (int)hipGetLastError();
+}
+
+// Epoch set-up of the fp64 CSR chains: every chain's double vector = w_in (GPU-wide, as
+// wf32_init_kernel; C5: 34 GB in ~5 ms).
+__global__ __launch_bounds__(256) void w64_init_kernel(double* __restrict__ wv, int64_t wstride_d,
+                                                       const double* __restrict__ w_in, int d,
+                                                       int n_chains, int chains_per_block) {
+    const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 2;
+    if (i >= d) return;
+    const bool full = i + 2 <= d;
+    const f64x2 v = full ? *reinterpret_cast<const f64x2*>(w_in + i) : f64x2{w_in[i], 0.0};
+    const int p0 = blockIdx.y * chains_per_block;
+    const int p1 = p0 + chains_per_block < n_chains ? p0 + chains_per_block : n_chains;
+    for (int p = p0; p < p1; ++p) {
+        double* dst = wv + (int64_t)p * wstride_d + i;
+        if (full) *reinterpret_cast<f64x2*>(dst) = v;
+        else dst[0] = v.x;
+    }
+}
+
+bool sparse64_path_applies(int layout, int compute, int updater, bool check_conv, bool alpha_ok) {
+    return layout == kCsr && compute == 0 && !check_conv &&
+           (updater == U_SIMPLE || (updater == U_SQUARED_L2 && alpha_ok));
+}
+
+template <typename S, int GRAD>
+static int sparse64_upd(const ChainLaunch& L, const KParams& kp, int upd, hipStream_t st) {
+    if (upd == U_SIMPLE)
+        hipLaunchKernelGGL((chain_sparse64<S, GRAD, U_SIMPLE>), dim3(kp.n_chains), dim3(64), 0, st, L, kp);
+    else
+        hipLaunchKernelGGL((chain_sparse64<S, GRAD, U_SQUARED_L2>), dim3(kp.n_chains), dim3(64), 0, st, L, kp);
+    return (int)hipGetLastError();
+}
+
+template <typename S>
+static int sparse64_grad(const ChainLaunch& L, const KParams& kp, int grad, int upd, hipStream_t st) {
+    switch (grad) {
+    case G_LOGISTIC: return sparse64_upd<S, G_LOGISTIC>(L, kp, upd, st);
+    case G_LEAST_SQUARES: return sparse64_upd<S, G_LEAST_SQUARES>(L, kp, upd, st);
+    case G_HINGE: return sparse64_upd<S, G_HINGE>(L, kp, upd, st);
+    default: return -3;
+    }
+}
+
+int launch_sparse64_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
+                           int updater, hipStream_t stream, int* kernel_variant) {
+    if (kp.n_chains <= 0) return 0;
+    if (!sparse64_path_applies(kCsr, 0, updater, false, kp.alpha_ok != 0)) return -3;
+    // the chain's f64 vector: [d] + [128] + [1024] doubles inside its slice of L.wf32
+    if (!L.wf32 || L.wstride < 2 * ((int64_t)kp.d + 128 + 1024) || (L.wstride & 3) || !L.walpha)
+        return (int)hipErrorInvalidValue;
+    const int bx = (kp.d + 511) / 512;
+    int by = (2048 + bx - 1) / bx;
+    by = by < kp.n_chains ? by : kp.n_chains;
+    const int per = (kp.n_chains + by - 1) / by;
+    by = (kp.n_chains + per - 1) / per;
+    hipLaunchKernelGGL(w64_init_kernel, dim3(bx, by), dim3(256), 0, stream, reinterpret_cast<double*>(L.wf32),
+                       L.wstride / 2, L.w_in, kp.d, kp.n_chains, per);
+    if (kernel_variant) *kernel_variant = 420 + storage;
+    if (storage == 1) return sparse64_grad<float>(L, kp, gradient, updater, stream);
+    return sparse64_grad<double>(L, kp, gradient, updater, stream);
 }
 
 int launch_sparse_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,

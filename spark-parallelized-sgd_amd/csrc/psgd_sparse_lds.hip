@@ -710,8 +710,11 @@ static int lds_depth() {
     return (e && atoi(e) == 8) ? 8 : 4;
 }
 
-bool sparse_lds_applies(int64_t d, int64_t max_nnz) {
-    if (max_nnz > LCAP) return false;
+// The chain, loader and tagger waves keep row numbers in 32 bits (psgd_sparse_lds.hip: n): a
+// partition of more than INT32_MAX rows (>= 32 GiB of 16-byte CSR rows, which fits in HBM) takes
+// chain_sparse / chain_general instead.
+bool sparse_lds_applies(int64_t d, int64_t max_nnz, int64_t n_max) {
+    if (max_nnz > LCAP || n_max > (int64_t)INT32_MAX) return false;
     return (lds_depth() == 8 ? lds_head<8, float>(d) : lds_head<4, float>(d)) >= 0;
 }
 
@@ -720,14 +723,14 @@ int64_t sparse_lds_head(int64_t d) { return lds_depth() == 8 ? lds_head<8, float
 int launch_sparse_lds_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
                              int updater, int64_t max_nnz, hipStream_t stream, int* kernel_variant) {
     if (kp.n_chains <= 0) return 0;
-    if (!sparse_lds_applies(kp.d, max_nnz)) return -3;
+    if (!sparse_lds_applies(kp.d, max_nnz, kp.n_max)) return -3;
     if (!L.wf32 || L.wstride < (int64_t)kp.d + 128 + 1024) return (int)hipErrorInvalidValue;
     if (lds_depth() == 8) return lds_launch<8, float>(L, kp, storage, gradient, updater, stream, kernel_variant);
     return lds_launch<4, float>(L, kp, storage, gradient, updater, stream, kernel_variant);
 }
 
-bool sparse_lds64_applies(int64_t d, int64_t max_nnz, int updater, bool check_conv, bool alpha_ok) {
-    if (max_nnz > LCAP || check_conv) return false;
+bool sparse_lds64_applies(int64_t d, int64_t max_nnz, int updater, bool check_conv, bool alpha_ok, int64_t n_max) {
+    if (max_nnz > LCAP || check_conv || n_max > (int64_t)INT32_MAX) return false;
     if (updater != U_SIMPLE && !(updater == U_SQUARED_L2 && alpha_ok)) return false;
     return (lds_depth() == 8 ? lds_head<8, double>(d) : lds_head<4, double>(d)) >= 0;
 }
@@ -735,7 +738,7 @@ bool sparse_lds64_applies(int64_t d, int64_t max_nnz, int updater, bool check_co
 int launch_sparse_lds64_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
                                int updater, int64_t max_nnz, hipStream_t stream, int* kernel_variant) {
     if (kp.n_chains <= 0) return 0;
-    if (!sparse_lds64_applies(kp.d, max_nnz, updater, false, kp.alpha_ok != 0)) return -3;
+    if (!sparse_lds64_applies(kp.d, max_nnz, updater, false, kp.alpha_ok != 0, kp.n_max)) return -3;
     // the chain's f64 vector: [d] + [128] + [1024] doubles inside its slice of L.wf32
     if (!L.wf32 || L.wstride < 2 * ((int64_t)kp.d + 128 + 1024) || (L.wstride & 3) || !L.w_out)
         return (int)hipErrorInvalidValue;

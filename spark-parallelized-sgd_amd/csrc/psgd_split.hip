@@ -479,8 +479,12 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
             T val[KV], nrm[KV];
             val[0] = wave_sum_uniform(acc);
             if constexpr (CONV) { val[1] = T(0); val[2] = T(0); }
-            publish(val, n);
-            collect(n, nrm);
+            // exchange index: n, or after a break at sample t, t + 1 -- its parity slot last held
+            // sample t - 1, which every wave has read (each published t after reading it); slot
+            // t & 1 may still be being polled for sample t by a slower wave
+            const int32_t fx = conv_at < n ? conv_at + 1 : n;
+            publish(val, fx);
+            collect(fx, nrm);
             if (count > 0) {
                 if constexpr (UPD == U_L1) {
                     rv = double(nrm[0]) * kp.reg;

@@ -209,10 +209,18 @@ class HipEngine(ShardedEngine):
         return self.ctx.initial_regval(params, w_host)
 
     def epoch(self, params, w_dev, with_counts: bool = False):
+        """The folded partial is written on `self.stream`. Its readers may be on any stream: the
+        caller's current stream is made to wait for the epoch before this returns, so a read
+        there (e.g. `.cpu()` on the default stream) sees the finished result -- never the
+        buffer's previous contents, which the driver would take for an empty batch (count 0,
+        ParallelizedSGD.scala:295-297)."""
+        caller = self.torch.cuda.current_stream(self.dev)
         # order after whatever produced the inputs on the caller's stream
-        self.stream.wait_stream(self.torch.cuda.current_stream(self.dev))
+        self.stream.wait_stream(caller)
         with self.torch.cuda.stream(self.stream):
-            return super().epoch(params, w_dev, with_counts)
+            out = super().epoch(params, w_dev, with_counts)
+        caller.wait_stream(self.stream)
+        return out
 
     def local_partial(self, params, w_dev, with_counts):
         # The lock serialises re-registration and the enqueue; the device order of epochs that
@@ -452,6 +460,34 @@ class DriverCheckpoint:
         self.path, self.every = str(path), int(every)
 
     def load(self, fingerprint: np.ndarray):
+        """The saved loop state, or None. With world > 1 only rank 0 reads the file (it is the
+        rank that writes it; other ranks may see a node-local path or none) and broadcasts the
+        state, so every rank resumes at the same iteration; a rank whose own parameter/data
+        fingerprint differs from rank 0's makes every rank raise, rather than issue mismatched
+        collectives. The fingerprint covers the parameters, the data's shape and the initial
+        weights, not the data's values."""
+        rank, world, _ = _dist()
+        state, err = None, None
+        if rank == 0:
+            try:
+                state = self._read(fingerprint)
+            except IllegalArgumentException as e:
+                err = str(e)
+        if world > 1:
+            import torch.distributed as dist
+            box = [(state, err, np.asarray(fingerprint).tobytes())]
+            dist.broadcast_object_list(box, src=0)
+            state, err, fp0 = box[0]
+            agree = [None] * world
+            dist.all_gather_object(agree, fp0 == np.asarray(fingerprint).tobytes())
+            if err is None and not all(agree):
+                err = (f"checkpoint {self.path}: ranks {[r for r, a in enumerate(agree) if not a]} "
+                       f"run with other parameters or data than rank 0")
+        if err is not None:
+            raise IllegalArgumentException(err)
+        return state
+
+    def _read(self, fingerprint: np.ndarray):
         import os
         if not os.path.exists(self.path):
             return None

@@ -58,6 +58,12 @@ def main():
                 got = folded.cpu().numpy()
                 res[name + "_single"] = single.cpu().numpy()
             res[name + "_rccl"] = got
+            # the same epoch read on the default stream, with no stream block (HipEngine.epoch
+            # makes the caller's stream wait for the engine's): the partial as it ends the epoch
+            eng._partial.fill_(-7.0)
+            torch.cuda.synchronize()
+            partial, _ = eng.epoch(prm, w)
+            res[name + "_default"] = partial.cpu().numpy()
         np.savez(out, **res)
     finally:
         dist.destroy_process_group()

@@ -44,3 +44,30 @@ def test_kernels_are_gfx950_code_objects(pkg):
     data = open(pkg._native.LIB_PATH, "rb").read()
     assert b"gfx950" in data
     assert b"chain_dense" in data and b"chain_general" in data and b"fold_kernel" in data
+
+
+def test_kernel_selection_limits_on_the_host(pkg):
+    """The dispatch predicates are host code (no device needed). chain_sparse_lds (fp32 and fp64)
+    counts a chain's rows in 32 bits, so a partition of more than INT32_MAX rows must not select
+    it (such partitions fit in HBM as 16-byte CSR rows); chain_sparse64 takes fp64 CSR
+    with Simple, or SquaredL2 while alpha stays in range, and never the per-sample break."""
+    lib = ctypes.CDLL(pkg._native.LIB_PATH)
+    lds = lib._ZN4psgd18sparse_lds_appliesElll
+    lds.restype, lds.argtypes = ctypes.c_bool, [ctypes.c_int64] * 3
+    lds64 = lib._ZN4psgd20sparse_lds64_appliesEllibbl
+    lds64.restype = ctypes.c_bool
+    lds64.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_bool, ctypes.c_bool, ctypes.c_int64]
+    s64 = lib._ZN4psgd21sparse64_path_appliesEiiibb
+    s64.restype = ctypes.c_bool
+    s64.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_bool, ctypes.c_bool]
+    big = 2**31 - 1
+    assert lds(47236, 94, big) and not lds(47236, 94, big + 1)
+    assert lds64(47236, 94, 0, False, True, big) and not lds64(47236, 94, 0, False, True, big + 1)
+    assert not lds(47236, 129, 100)              # rows of more than 128 entries
+    CSR, DENSE, F64, F32 = 1, 0, 0, 1
+    SIMPLE, L2, L1 = 0, 1, 2
+    assert s64(CSR, F64, SIMPLE, False, False) and s64(CSR, F64, L2, False, True)
+    assert not s64(CSR, F64, L2, False, False)   # alpha out of range: chain_general renormalises
+    assert not s64(CSR, F64, SIMPLE, True, True)  # per-sample break: chain_general
+    assert not s64(CSR, F32, SIMPLE, False, True) and not s64(DENSE, F64, SIMPLE, False, True)
+    assert not s64(CSR, F64, L1, False, True)

@@ -149,7 +149,7 @@ def test_two_ranks_match_single_process_oracle(tmp_path, oracle, pkg, P):
         assert np.array_equal(res["w"], w) and np.array_equal(res["h"], h)
 
 
-def _ckpt_worker(rank, world, port, ck, stop, result_path):
+def _ckpt_worker(rank, world, port, ck, stop, result_path, w0_shift=0.0):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -165,8 +165,16 @@ def _ckpt_worker(rank, world, port, ck, stop, result_path):
         y = (rng.uniform(size=n) > 0.5).astype(float)
         data = pkg.PartitionedData.parallelize(y, X, 4)
         eng = make_oracle_engine(pkg, O)(data, rank, world)
-        w, h = pkg.runParallelizedSGD(data, pkg.LogisticGradient(), pkg.SquaredL2SGDUpdater(), 0.5, stop,
-                                      0.01, 1.0, np.zeros(d), 0.0, engine=eng, checkpoint=ck)
+        if isinstance(ck, (list, tuple)):   # per-rank paths (a node-local checkpoint directory)
+            ck = ck[rank]
+        w0 = np.zeros(d) + (w0_shift if rank == 1 else 0.0)
+        try:
+            w, h = pkg.runParallelizedSGD(data, pkg.LogisticGradient(), pkg.SquaredL2SGDUpdater(), 0.5, stop,
+                                          0.01, 1.0, w0, 0.0, engine=eng, checkpoint=ck)
+        except pkg.IllegalArgumentException as e:
+            if result_path:
+                np.savez(f"{result_path}.rank{rank}.err", msg=str(e))
+            return
         dist.barrier()   # rank 0's checkpoint is on disk before any rank resumes from it
         if rank == 0 and result_path:
             np.savez(result_path, w=w, h=h)
@@ -186,3 +194,25 @@ def test_two_ranks_checkpoint_resume(tmp_path):
     mp.start_processes(_ckpt_worker, args=(world, _free_port(), ck, 5, res), nprocs=world, start_method="spawn")
     a, b = np.load(full), np.load(res)
     assert len(a["h"]) == 5 and np.array_equal(a["w"], b["w"]) and np.array_equal(a["h"], b["h"])
+
+
+def test_two_ranks_checkpoint_rank0_broadcast(tmp_path):
+    """Resume reads the checkpoint on rank 0 only and broadcasts it: rank 1's path
+    holds no file (a node-local directory) and the resumed run still equals the uninterrupted
+    one; a rank whose parameters differ from rank 0's makes both ranks raise."""
+    world = 2
+    full, res = str(tmp_path / "full.npz"), str(tmp_path / "res.npz")
+    mp.start_processes(_ckpt_worker, args=(world, _free_port(), str(tmp_path / "a.npz"), 5, full),
+                       nprocs=world, start_method="spawn")
+    paths = [str(tmp_path / "r0.npz"), str(tmp_path / "elsewhere" / "r1.npz")]
+    mp.start_processes(_ckpt_worker, args=(world, _free_port(), paths, 2, ""), nprocs=world, start_method="spawn")
+    assert not os.path.exists(paths[1])
+    mp.start_processes(_ckpt_worker, args=(world, _free_port(), paths, 5, res), nprocs=world, start_method="spawn")
+    a, b = np.load(full), np.load(res)
+    assert np.array_equal(a["w"], b["w"]) and np.array_equal(a["h"], b["h"])
+    bad = str(tmp_path / "bad.npz")
+    mp.start_processes(_ckpt_worker, args=(world, _free_port(), paths, 5, bad, 0.25), nprocs=world,
+                       start_method="spawn")
+    for r in range(world):
+        msg = str(np.load(f"{bad}.rank{r}.err.npz")["msg"])
+        assert "other parameters or data than rank 0" in msg, msg

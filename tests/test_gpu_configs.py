@@ -168,7 +168,7 @@ def c5():
     return d, rp, col, val, y, offs, w0
 
 
-@pytest.mark.parametrize("compute,want", [("f32", 401), ("f64", 201)])
+@pytest.mark.parametrize("compute,want", [("f32", 401), ("f64", 420)])
 def test_c5_wide_sparse_l2(pkg, oracle, c5, compute, want):
     # f32: chain_sparse (HBM-resident weights); f64: chain_general's alpha-scaled lazy SquaredL2
     d, rp, col, val, y, offs, w0 = c5
@@ -321,6 +321,40 @@ def test_rccl_exchange_single_rank(tmp_path):
         single, rccl = res[name + "_single"], res[name + "_rccl"]
         assert np.isfinite(single).all() and single[-1] > 0, name
         assert np.array_equal(single, rccl), name
+        assert np.array_equal(single, res[name + "_default"]), name + " read on the default stream"
+
+
+def test_epoch_result_on_default_stream(pkg):
+    """HipEngine.epoch returns tensors written on the engine's stream; a caller that reads them on
+    its own (default) stream, with no stream block, must see the finished epoch (a
+    CSR fp32 partial once came back all zeros with count 0, which the driver would take for an
+    empty batch and skip the update, ParallelizedSGD.scala:295-297). The partial buffer is
+    poisoned first and the chains run long enough (256 chains x 4,000 rows) that an unordered
+    read would see the poison."""
+    import torch
+    rng = np.random.default_rng(9)
+    n, d, P, k = 1_024_000, 40_000, 256, 32
+    rp = np.arange(n + 1, dtype=np.int64) * k
+    col = np.sort(rng.choice(d - k, size=(n, k)), axis=1) + np.arange(k)[None, :]
+    col = col.astype(np.int32).reshape(-1)
+    val = rng.standard_normal(n * k).astype(np.float32)
+    y = (rng.uniform(size=n) > 0.5).astype(np.float64)
+    offs = [i * n // P for i in range(P + 1)]
+    data = pkg.PartitionedData([pkg.CsrPartition(y[a:b], rp[a:b + 1] - rp[a], col[rp[a]:rp[b]], val[rp[a]:rp[b]], d)
+                                for a, b in zip(offs[:-1], offs[1:])])
+    eng = pkg.HipEngine(data, 0, 1, device=0)
+    prm = pkg.make_params(pkg.HingeGradient(), pkg.SimpleSGDUpdater(), 0.5, 0.0, 1.0, 0.0, "f32")
+    w = eng.weights(np.zeros(d))
+    ref = None
+    for _ in range(3):
+        eng._partial.fill_(-7.0)
+        torch.cuda.synchronize()
+        partial, _ = eng.epoch(prm, w)
+        got = partial.cpu().numpy()          # the default stream, no stream block
+        assert got[-1] == n, got[-3:]
+        torch.cuda.synchronize()
+        ref = got if ref is None else ref
+        assert np.array_equal(got, ref)
 
 
 @pytest.fixture(scope="module")
@@ -341,11 +375,11 @@ def c5_full_chains(oracle):
     return d, rp, col, val, y, offs, ref
 
 
-@pytest.mark.parametrize("compute,want", [("f32", 401), ("f64", 201)])
+@pytest.mark.parametrize("compute,want", [("f32", 401), ("f64", 420)])
 def test_c5_1024_chains(pkg, c5_full_chains, compute, want):
     """C5 at its real chain count: wf32_init_kernel over 1,024 chains x 2^22 features, the
-    chains, fold_f32_kernel over 1,024 fp32 vectors (f32); chain_general's alpha-scaled lazy
-    SquaredL2 and fold_kernel over 1,024 f64 vectors (f64). Against the oracle: counts exact,
+    chains, fold_f32_kernel over 1,024 fp32 vectors (f32); w64_init_kernel, chain_sparse64's
+    alpha-scaled SquaredL2 and the fold over 1,024 f64 vectors (f64). Against the oracle: counts exact,
     fp64 at 1e-9, fp32 at its stated tolerance."""
     d, rp, col, val, y, offs, (wr, hr, cr) = c5_full_chains
     vs = val.astype(np.float32) if compute == "f32" else val
@@ -360,3 +394,23 @@ def test_c5_1024_chains(pkg, c5_full_chains, compute, want):
     else:
         assert_close(w, wr, what="c5 1024 chains fp64 weights")
         assert_close(h, hr, what="c5 1024 chains fp64 loss")
+
+
+def test_bench_two_ranks_gloo():
+    """bench.py's multi-rank path -- the placeholder partitions of the other rank, the n * world
+    count check, the prewarm MAX agreement, the world > 1 timing and the cross-rank all-gather +
+    fold -- run with two ranks sharing cuda:0 over gloo (RCCL refuses two ranks on one device;
+    the driver's 8-GPU node runs the nccl form). The line reports both ranks' samples."""
+    import json
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
+           "--rows", "200000", "--secondary", "", "--steps", "3", "--warmup", "1", "--prewarm-s", "0.2"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 3 and out["warmup"] == 1
+    assert out["config"]["parallelism"].startswith("dp2"), out["config"]
+    assert out["value"] > 0 and out["prewarm"]["epochs"] >= 2
+    # both ranks' rows were counted: value = 2 * 200,000 samples per step / the step time
+    assert abs(out["value"] * out["ms_per_step"] / 1e3 - 400_000) < 1.0, out

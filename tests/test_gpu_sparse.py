@@ -172,12 +172,14 @@ def test_sparse_device_registration(pkg, oracle):
 
 
 # ------------------------------------------------------------------------------------------
-# fp64 compute (the parity mode) on chain_sparse_lds<., double>: 1e-9 and exact counts.
+# fp64 compute (the parity mode) on chain_sparse_lds<., double> and chain_sparse64 (rows wider than
+# 128 entries, d past the LDS kernel's reach, or forced): 1e-9 and exact counts.
 # ------------------------------------------------------------------------------------------
 KERNELS64 = {  # name: (environment, variant base without the storage digit)
     "lds64": ({}, 620),
     "lds64_tail": ({"PSGD_SPARSE_LDS_HEAD": "third"}, 620),
     "lds64_tail_sk8": ({"PSGD_SPARSE_LDS_HEAD": "third", "PSGD_SPARSE_SK": "8"}, 630),
+    "hbm64": ({"PSGD_SPARSE_KERNEL": "hbm64"}, 420),   # chain_sparse64: weights as doubles in HBM
 }
 
 
@@ -206,7 +208,7 @@ def check64(pkg, oracle, rp, col, val, y, d, offs, grad, upd, step, reg, iters, 
                                           return_chain_counts=True)
     if want is None:
         wide = int(np.max(np.diff(rp))) > 128
-        want = 201 if wide else base + (1 if dtype == np.float32 else 0)
+        want = (420 if wide else base) + (1 if dtype == np.float32 else 0)
     assert pkg.optimization.get_context(0).last_kernel() == want
     mat = oracle.Matrix(y, row_ptr=rp, col=col, val=vstore.astype(np.float64), d=d)
     wr, hr, cr = oracle.run(mat, offs, grad, upd, step, iters, reg, np.zeros(d), tol=0.0, fraction=frac,
@@ -255,3 +257,27 @@ def test_sparse_fp64_alpha_out_of_range_takes_chain_general(pkg, oracle):
     n, d = 600, 300
     rp, col, val, y = synth_csr(rng, n, d, 1, 20, "logistic")
     check64(pkg, oracle, rp, col, val, y, d, [0, 300, 600], "logistic", "squared_l2", 1.0, 1.0, 2, want=201)
+
+
+@pytest.mark.parametrize("upd", ["simple", "squared_l2"])
+def test_sparse_fp64_rows_wider_than_128(pkg, oracle, upd):
+    """Rows of 100-300 entries: chain_sparse64's per-lane loop past two entries (gathers, dot and
+    stores), both storage dtypes."""
+    rng = np.random.default_rng(27)
+    n, d = 400, 1000
+    rp, col, val, y = synth_csr(rng, n, d, 100, 300, "logistic")
+    for dtype in (np.float64, np.float32):
+        check64(pkg, oracle, rp, col, val, y, d, [0, 200, 400], "logistic", upd, 0.5, 0.02, 2, dtype=dtype)
+
+
+@pytest.mark.parametrize("grad", ["least_squares", "logistic", "hinge"])
+def test_sparse_fp64_beyond_lds(pkg, oracle, grad):
+    """d = 200,000: past the fp64 LDS kernel's ~61k features, so chain_sparse64 (weights as
+    doubles in HBM) runs by default; SquaredL2 (alpha-scaled) and Simple, ragged and empty
+    partitions, f32 and f64 rows."""
+    rng = np.random.default_rng(31 + len(grad))
+    n, d = 3000, 200_000
+    rp, col, val, y = synth_csr(rng, n, d, 0, 120, grad)
+    offs = [0, 1000, 1000, 1001, 2200, 3000]
+    check64(pkg, oracle, rp, col, val, y, d, offs, grad, "squared_l2", 0.4, 0.01, 3, want=420)
+    check64(pkg, oracle, rp, col, val, y, d, offs, grad, "simple", 0.4, 0.0, 2, dtype=np.float32, want=421)

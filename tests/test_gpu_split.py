@@ -132,3 +132,32 @@ def test_split_per_sample_convergence(pkg, oracle, grad, upd, d, storage, tol):
     assert [list(c) for c in counts] == [list(c) for c in cr[: len(counts)]], tag
     assert_close(w, wr, what=tag + " weights")
     assert_close(h, hr, what=tag + " loss")
+
+
+@pytest.mark.parametrize("upd", ["l1", "squared_l2"])
+@pytest.mark.parametrize("d,storage", [(1024, np.float32), (256, np.float64)])
+def test_split_break_same_parity_final_exchange(pkg, oracle, upd, d, storage):
+    """The regVal exchange after a per-sample break: a chain that breaks at sample t
+    with t = n (mod 2) must not publish its final norms into slot t & 1, which a slower wave may
+    still be polling for sample t. Many short chains of ragged lengths (37 / 38 rows) at a tol that
+    breaks most of them early: both parities of the break against n occur, every chain's count is
+    exact and the run finishes (no watchdog)."""
+    rng = np.random.default_rng(4242 + d)
+    P = 128
+    n = P * 37 + 61
+    X, y = synth(rng, n, d, "logistic")
+    reg = {"l1": 0.002, "squared_l2": 0.05}[upd]
+    tol = 0.05
+    data = pkg.PartitionedData.parallelize(y, X.astype(storage), P, dtype=storage)
+    offs = [i * n // P for i in range(P)] + [n]
+    sizes = np.diff(offs)
+    w, h, counts = pkg.runParallelizedSGD(data, pkg.LogisticGradient(), getattr(pkg, U[upd])(), 0.5, 3,
+                                          reg, 1.0, np.zeros(d), tol, return_chain_counts=True)
+    wr, hr, cr = oracle.run(oracle.Matrix(y, X.astype(np.float64)), offs, "logistic", upd, 0.5, 3, reg,
+                            np.zeros(d), tol=tol, n_threads=8)
+    assert [list(c) for c in counts] == [list(c) for c in cr[: len(counts)]]
+    same = sum(int(c < s and c % 2 == s % 2) for it in cr for c, s in zip(it, sizes))
+    other = sum(int(c < s and c % 2 != s % 2) for it in cr for c, s in zip(it, sizes))
+    assert same > 0 and other > 0, (same, other)
+    assert_close(w, wr, what=f"{upd} break-parity weights")
+    assert_close(h, hr, what=f"{upd} break-parity loss")

@@ -14,7 +14,9 @@
 // DEPTH rows' gathers are in flight before the group's stores (DEPTH = 1: each row's stores
 // wait for its own gathers, the chain's dependence; deeper: independent rows, the rate a deeper
 // pipeline could reach). The best rate over the depths is the pattern's ceiling on this chip.
-// Usage: gather_bench [rows per chain = 20000] [chains = 1024] [d = 4194304]
+// ELEM = 8 (4th argument): the same pattern on 8-byte words (global_load_dwordx2 ... sc1 /
+// global_store_dwordx2), c5's fp64 chain (chain_sparse64) -- a 34 GB footprint.
+// Usage: gather_bench [rows per chain = 20000] [chains = 1024] [d = 4194304] [elem bytes = 4]
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -32,28 +34,39 @@ __device__ __forceinline__ float gather(const float* p) {
     else asm volatile("global_load_dword %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
     return v;
 }
+template <int MODE>
+__device__ __forceinline__ double gather(const double* p) {
+    double v;
+    if constexpr (MODE == 3) asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    else asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+// POL: 0 plain, 1 nt, 2 sc1
+template <int POL>
 __device__ __forceinline__ void store(float* p, float v) {
-    asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");
+    if constexpr (POL == 1) asm volatile("global_store_dword %0, %1, off nt" : : "v"(p), "v"(v) : "memory");
+    else if constexpr (POL == 2) asm volatile("global_store_dword %0, %1, off sc1" : : "v"(p), "v"(v) : "memory");
+    else asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");
 }
-__device__ __forceinline__ void store_nt(float* p, float v) {
-    asm volatile("global_store_dword %0, %1, off nt" : : "v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ void store_sc1(float* p, float v) {
-    asm volatile("global_store_dword %0, %1, off sc1" : : "v"(p), "v"(v) : "memory");
+template <int POL>
+__device__ __forceinline__ void store(double* p, double v) {
+    if constexpr (POL == 1) asm volatile("global_store_dwordx2 %0, %1, off nt" : : "v"(p), "v"(v) : "memory");
+    else if constexpr (POL == 2) asm volatile("global_store_dwordx2 %0, %1, off sc1" : : "v"(p), "v"(v) : "memory");
+    else asm volatile("global_store_dwordx2 %0, %1, off" : : "v"(p), "v"(v) : "memory");
 }
 
-template <int MODE, int DEPTH>
-__global__ __launch_bounds__(64) void gather_store(float* W, long stride, int rows, unsigned width, int nnz) {
+template <typename E, int MODE, int DEPTH>
+__global__ __launch_bounds__(64) void gather_store(E* W, long stride, int rows, unsigned width, int nnz) {
     const int lane = threadIdx.x;
-    float* base = W + (long)blockIdx.x * stride;
+    E* base = W + (long)blockIdx.x * stride;
     const unsigned key = mix(blockIdx.x * 0x9E3779B9u + 12345u);
     // inactive lanes (entries >= nnz) use a private dummy word past the vector, as the product does
-    float* dummy = base + (long)width * nnz + lane;
-    float acc = 0.0f;
+    E* dummy = base + (long)width * nnz + lane;
+    E acc = 0;
     for (int r = 0; r < rows; r += DEPTH) {
-        float* p0[DEPTH];
-        float* p1[DEPTH];
-        float g0[DEPTH], g1[DEPTH];
+        E* p0[DEPTH];
+        E* p1[DEPTH];
+        E g0[DEPTH], g1[DEPTH];
 #pragma unroll
         for (int q = 0; q < DEPTH; ++q) {
             const unsigned h = mix(key ^ (unsigned)(r + q) * 0x85EBCA6Bu);
@@ -63,37 +76,32 @@ __global__ __launch_bounds__(64) void gather_store(float* W, long stride, int ro
                 g0[q] = gather<MODE>(p0[q]);
                 g1[q] = gather<MODE>(p1[q]);
             } else {
-                g0[q] = g1[q] = 1.0f;
+                g0[q] = g1[q] = E(1);
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
         for (int q = 0; q < DEPTH; ++q) {
-            if constexpr (MODE == 4) {
-                store_nt(p0[q], g0[q] + 1.0f);
-                store_nt(p1[q], g1[q] + 1.0f);
-            } else if constexpr (MODE == 5) {
-                store_sc1(p0[q], g0[q] + 1.0f);
-                store_sc1(p1[q], g1[q] + 1.0f);
-            } else if constexpr (MODE != 1) {
-                store(p0[q], g0[q] + 1.0f);
-                store(p1[q], g1[q] + 1.0f);
+            if constexpr (MODE != 1) {
+                constexpr int POL = MODE == 4 ? 1 : MODE == 5 ? 2 : 0;
+                store<POL>(p0[q], g0[q] + E(1));
+                store<POL>(p1[q], g1[q] + E(1));
             }
             acc += g0[q] + g1[q];
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (acc == 12345.678f) base[0] = acc;
+    if (acc == E(12345.678)) base[0] = acc;
 }
 
-template <int MODE, int DEPTH>
-static float run(float* W, long stride, int rows, int chains, unsigned width, int nnz) {
+template <typename E, int MODE, int DEPTH>
+static float run(E* W, long stride, int rows, int chains, unsigned width, int nnz) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
     float best = 1e30f;
     for (int it = 0; it < 3; ++it) {
         CK(hipEventRecord(a));
-        hipLaunchKernelGGL((gather_store<MODE, DEPTH>), dim3(chains), dim3(64), 0, 0, W, stride, rows, width, nnz);
+        hipLaunchKernelGGL((gather_store<E, MODE, DEPTH>), dim3(chains), dim3(64), 0, 0, W, stride, rows, width, nnz);
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
         float ms;
@@ -103,18 +111,16 @@ static float run(float* W, long stride, int rows, int chains, unsigned width, in
     return best;
 }
 
-int main(int argc, char** argv) {
-    const int rows = argc > 1 ? atoi(argv[1]) : 20000;
-    const int chains = argc > 2 ? atoi(argv[2]) : 1024;
-    const unsigned d = argc > 3 ? (unsigned)atol(argv[3]) : (1u << 22);
+template <typename E>
+static void run_all(int rows, int chains, unsigned d) {
     const int nnz = 100;
     const unsigned width = d / nnz;
-    const long stride = ((long)d + 1152 + 63) / 64 * 64;   // as the product's wf32 stride
-    float* W;
-    CK(hipMalloc(&W, (size_t)chains * stride * 4));
-    CK(hipMemset(W, 0, (size_t)chains * stride * 4));
-    printf("gather_bench: %d chains x %d rows x %d entries, d = %u (%.1f GB of weights)\n", chains, rows, nnz,
-           d, (double)chains * stride * 4 / 1e9);
+    const long stride = ((long)d + 1152 + 63) / 64 * 64;   // as the product's wf32 stride (in elements)
+    E* W;
+    CK(hipMalloc(&W, (size_t)chains * stride * sizeof(E)));
+    CK(hipMemset(W, 0, (size_t)chains * stride * sizeof(E)));
+    printf("gather_bench: %d chains x %d rows x %d entries of %d bytes, d = %u (%.1f GB of weights)\n", chains,
+           rows, nnz, (int)sizeof(E), d, (double)chains * stride * sizeof(E) / 1e9);
     const double R = (double)rows * chains;
     const char* names[6] = {"gather sc1 + store (c5)", "gather sc1 only", "store only", "gather plain + store",
                             "store only (nt)", "store only (sc1)"};
@@ -123,9 +129,20 @@ int main(int argc, char** argv) {
                R / ms / 1e3, R * (mode == 0 || mode == 3 ? 2 : 1) * nnz / ms / 1e6);
     };
 #define RUN(M) \
-    report(M, 1, run<M, 1>(W, stride, rows, chains, width, nnz)); \
-    report(M, 4, run<M, 4>(W, stride, rows, chains, width, nnz)); \
-    report(M, 16, run<M, 16>(W, stride, rows, chains, width, nnz));
+    report(M, 1, run<E, M, 1>(W, stride, rows, chains, width, nnz)); \
+    report(M, 4, run<E, M, 4>(W, stride, rows, chains, width, nnz)); \
+    report(M, 16, run<E, M, 16>(W, stride, rows, chains, width, nnz));
     RUN(0) RUN(1) RUN(2) RUN(3) RUN(4) RUN(5)
+#undef RUN
+    CK(hipFree(W));
+}
+
+int main(int argc, char** argv) {
+    const int rows = argc > 1 ? atoi(argv[1]) : 20000;
+    const int chains = argc > 2 ? atoi(argv[2]) : 1024;
+    const unsigned d = argc > 3 ? (unsigned)atol(argv[3]) : (1u << 22);
+    const int elem = argc > 4 ? atoi(argv[4]) : 4;
+    if (elem == 8) run_all<double>(rows, chains, d);
+    else run_all<float>(rows, chains, d);
     return 0;
 }

@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-3 profiles for profiles/: per workload, one rocprofv3 kernel-trace + stats pass and
+# Profiles for profiles/: per workload, one rocprofv3 kernel-trace + stats pass and
 # separate FETCH_SIZE / WRITE_SIZE PMC passes (MI355X_MICROARCH.md §HBM), of the bench command
 # for that line (bench.py --secondary= ...). Summarised locally by tools/pmc_summary.py.
-# usage: tools/profile_r03.sh name1 name2 ...   (names below; default: all)
+# usage: tools/profile.sh name1 name2 ...   (names below; default: all; PROF_OUT = output dir)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/prof_r03
+OUT=${PROF_OUT:-gpurun_out/prof}
 mkdir -p $OUT
 declare -A ARGS=(
   [c2]="--workload c2"
@@ -15,7 +15,10 @@ declare -A ARGS=(
   [c3_f64rows]="--workload c3 --compute f64 --storage f64"
   [c4_f32]="--workload c4"
   [c4_f64]="--workload c4 --compute f64"
+  [c4_f64rows]="--workload c4 --compute f64 --storage f64"
   [c5]="--workload c5 --rows 20000000"
+  [c5_f64]="--workload c5 --compute f64 --rows 20000000"
+  [c5_f64rows]="--workload c5 --compute f64 --storage f64 --rows 20000000"
   [c3_f32_adagrad]="--workload c3 --updater adagrad"
   [c3_f32_adam]="--workload c3 --updater adam"
   [c3_f64_adagrad]="--workload c3 --compute f64 --updater adagrad"
