@@ -325,6 +325,20 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
             publish(val, t);
         }
         SPLIT_STAMP(st_dot);
+        // the sample's scalars that do not depend on its dot, before the exchange's wait (the spin
+        // is a branch: nothing after it is moved above it)
+        const T a_s = -s;
+        const bool first = t == 0;
+        const T iter = T(t + 1);
+        T al = T(0);
+        if constexpr (UPD == U_ADAM) {
+            if constexpr (sizeof(T) == 4) al = -(s / (T(1) - pow_fast(T(kp.beta), iter)));
+            // fp64: 1 - beta^iter as 1.0 once beta^iter <= 2^-54 (bit-identical, no library pow
+            // per sample on the chain) and the division by rcp + one Newton step
+            else al = -(s * recip_newton(one_minus_pow_iter(T(kp.beta), iter)));
+        }
+        [[maybe_unused]] const T shrink = T(kp.reg) * s;          // L1 (UPD.scala:133)
+        [[maybe_unused]] const T l2c = T(1) - s * T(kp.reg);      // SquaredL2 (UPD.scala:169)
 
         const char* next_ptr = slot_ptr + ROW_BYTES;
         if (next_ptr == ring_end) next_ptr = ring;
@@ -375,16 +389,6 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
             }
         }
 
-        const T a_s = -s;
-        const bool first = t == 0;
-        const T iter = T(t + 1);
-        T al = T(0);
-        if constexpr (UPD == U_ADAM) {
-            if constexpr (sizeof(T) == 4) al = -(s / (T(1) - pow_fast(T(kp.beta), iter)));
-            // fp64: 1 - beta^iter as 1.0 once beta^iter <= 2^-54 (bit-identical, no library pow
-            // per sample on the chain) and the division by rcp + one Newton step
-            else al = -(s * recip_newton(one_minus_pow_iter(T(kp.beta), iter)));
-        }
         T2 dsq2 = T2{T(0), T(0)}, nsq2 = T2{T(0), T(0)};
 #pragma unroll
         for (int e = 0; e < E2; ++e) {
@@ -403,15 +407,13 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
                     nw.y = old.y + a_s * (g.y * rsqrt_newton(acc2.y + T(1)));
                 }
             } else if constexpr (UPD == U_SQUARED_L2) {
-                const T c = T(1) - s * T(kp.reg);
-                nw = old * c;                       // brzWeights :*= (1 - s*lambda) (UPD.scala:172)
+                nw = old * l2c;                     // brzWeights :*= (1 - s*lambda) (UPD.scala:172)
                 nw = nw + a_s * (mult * x[e]);      // axpy(-s, grad, w)
             } else if constexpr (UPD == U_SIMPLE) {
                 if constexpr (sizeof(T) == 4) nw = __builtin_elementwise_fma(T2{a_s * mult, a_s * mult}, x[e], old);
                 else nw = old + a_s * (mult * x[e]);   // the reference's two roundings (UPD.scala:95)
             } else if constexpr (UPD == U_L1) {
                 // axpy(-s, grad, w), then soft thresholding by regParam * s (UPD.scala:133-146)
-                const T shrink = T(kp.reg) * s;
                 nw = old + a_s * (mult * x[e]);
                 nw.x = jsignum(nw.x) * jmax(T(0), m_fabs(nw.x) - shrink);
                 nw.y = jsignum(nw.y) * jmax(T(0), m_fabs(nw.y) - shrink);
