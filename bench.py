@@ -116,8 +116,7 @@ def kernel_name(variant):
     if 600 <= variant < 700:
         prec = "fp64" if (variant % 100) >= 20 else "fp32"
         return (f"chain_sparse_lds ({prec} CSR chain, weights LDS-resident [tail past ~160 KiB: L2-resident, "
-                f"gathered {6 if (variant % 20) >= 10 else 4} + 1 samples ahead by a tail wave, with an LDS "
-                f"feature-tag correction; the chain wave issues no VMEM])")
+                f"gathered {8 if (variant % 20) >= 10 else 4} samples ahead with an LDS feature-tag correction])")
     if 420 <= variant < 430:
         return ("chain_sparse64 (fp64 CSR chain, weights as double vectors in HBM, alpha-scaled SquaredL2, "
                 "one gather round trip per sample)")

@@ -1057,29 +1057,29 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         HIP_TRY(hipEventRecord(ctx->ev_end, st));
         ctx->ev_recorded = (e == 0);
         if (L.stamps) {   // PSGD_STAMPS=1: per-chain cycle counters of the CSR fp32 kernels (stderr)
-            // chain_sparse_lds: {chain, loader, tagger, tail} x {total, waiting}; chain_sparse_spec:
+            // chain_sparse_lds: {chain, loader, tagger} x {total, waiting}; chain_sparse_spec:
             // {chain, helper} x {total, waiting}
             // chain_split: {total, row + dot + reduce, exchange wait, multiplier + update} per
             // compute wave
             const bool split = ctx->last_variant >= 800;
-            const int KS = split ? 16 : ctx->last_variant >= 600 ? 8 : 4;
+            const int KS = split ? 16 : ctx->last_variant >= 600 ? 6 : 4;
+            const int KST = split ? 16 : KS;   // stride per chain
             std::vector<unsigned long long> h((size_t)P * 16);
             HIP_TRY(hipMemcpyAsync(h.data(), L.stamps, h.size() * 8, hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
             std::vector<double> v[16];
             for (int p = 0; p < P; ++p)
                 for (int k = 0; k < KS; ++k)
-                    v[k].push_back((double)h[(size_t)p * KS + k] / std::max<int64_t>(n_max, 1));
+                    v[k].push_back((double)h[(size_t)p * KST + k] / std::max<int64_t>(n_max, 1));
             const char* n4[4] = {"chain.total", "chain.wait", "helper.total", "helper.wait"};
-            const char* n6[8] = {"chain.total", "chain.wait", "loader.total", "loader.wait", "tagger.total", "tagger.wait",
-                                 "tail.total", "tail.wait"};
+            const char* n6[6] = {"chain.total", "chain.wait", "loader.total", "loader.wait", "tagger.total", "tagger.wait"};
             const char* ns[4] = {"total", "dot", "xwait", "update"};
             for (int k = 0; k < KS; ++k) {
                 std::sort(v[k].begin(), v[k].end());
                 char nm[32];
                 if (split) snprintf(nm, sizeof nm, "wave%d.%s", k / 4, ns[k % 4]);
                 fprintf(stderr, "psgd stamps %-18s cycles/row median %8.1f\n",
-                        split ? nm : KS == 8 ? n6[k] : n4[k], v[k][v[k].size() / 2]);
+                        split ? nm : KS == 6 ? n6[k] : n4[k], v[k][v[k].size() / 2]);
             }
         }
         if (e == -2) return fail(PSGD_EUNSUPPORTED, "this gradient/updater/layout combination is not built");

@@ -2,7 +2,7 @@
 
 Every case runs on each kernel variant (PSGD_SPARSE_KERNEL forces one): chain_sparse_lds with
 all weights in LDS, with an LDS head of d/3 features and the rest in HBM (PSGD_SPARSE_LDS_HEAD:
-exercises the tail wave's gathers and the corrections at small d) at speculation depths 4 and 6,
+exercises the tail gathers and their corrections at small d) at speculation depths 4 and 8,
 chain_sparse_spec, and chain_sparse.
 
 fp32 compute is the throughput mode; its stated tolerance is weights within
@@ -37,7 +37,7 @@ def need_gpu():
 KERNELS = {  # name: (environment, variant base without the storage digit)
     "lds": ({"PSGD_SPARSE_KERNEL": "lds"}, 600),
     "lds_tail": ({"PSGD_SPARSE_KERNEL": "lds", "PSGD_SPARSE_LDS_HEAD": "third"}, 600),
-    "lds_tail_sk6": ({"PSGD_SPARSE_KERNEL": "lds", "PSGD_SPARSE_LDS_HEAD": "third", "PSGD_SPARSE_SK": "6"}, 610),
+    "lds_tail_sk8": ({"PSGD_SPARSE_KERNEL": "lds", "PSGD_SPARSE_LDS_HEAD": "third", "PSGD_SPARSE_SK": "8"}, 610),
     "spec": ({"PSGD_SPARSE_KERNEL": "spec"}, 410),
     "plain": ({"PSGD_SPARSE_KERNEL": "plain"}, 400),
 }
@@ -178,7 +178,7 @@ def test_sparse_device_registration(pkg, oracle):
 KERNELS64 = {  # name: (environment, variant base without the storage digit)
     "lds64": ({}, 620),
     "lds64_tail": ({"PSGD_SPARSE_LDS_HEAD": "third"}, 620),
-    "lds64_tail_sk6": ({"PSGD_SPARSE_LDS_HEAD": "third", "PSGD_SPARSE_SK": "6"}, 630),
+    "lds64_tail_sk8": ({"PSGD_SPARSE_LDS_HEAD": "third", "PSGD_SPARSE_SK": "8"}, 630),
     "hbm64": ({"PSGD_SPARSE_KERNEL": "hbm64"}, 420),   # chain_sparse64: weights as doubles in HBM
 }
 

@@ -16,40 +16,40 @@
 // (kp.alpha_ok); otherwise chain_general, which renormalises, runs.
 //
 // One workgroup = one chain = one CU (the 160 KiB LDS holds one chain's weights). Features
-// [0, K) live in LDS as fp32 ("head"); when d does not fit, features [K, d) ("tail") stay in the
-// chain's fp32 vector in HBM (L.wf32), 4 (d - K) bytes per chain instead of 4 d -- at rcv1 shape
-// (d = 47,236) ~100 KB, so 32 chains per XCD fit its 4 MiB L2 where whole vectors did not.
+// [0, K) live in LDS ("head"); when d does not fit, features [K, d) ("tail") stay in the chain's
+// vector in HBM (L.wf32), 4 (d - K) bytes per chain instead of 4 d -- at rcv1 shape (d = 47,236)
+// ~100 KB, so 32 chains per XCD fit its 4 MiB L2 where whole vectors did not.
 //   * head entries: the chain reads w_j from LDS at the sample and writes the new value back
 //     (one wave's LDS operations execute in program order, so row t+1 reads row t's update);
-//   * tail entries: gathered from HBM SK samples ahead (sc1 loads: L2 sees this wave's earlier
-//     stores first) and corrected as in chain_sparse_spec: a per-feature tag table over the tail
-//     (2 B per tail feature: (row & 255) << 8 | entry of the latest row holding the feature)
-//     names the latest of the SK preceding rows with the same feature, whose new value the chain
-//     left in that row's LDS slot in place of x_j. Tags never alias: the tagger sweeps 1/128 of
-//     the table per row and clears tags older than SK rows, so no tag outlives 256 rows.
-// Three waves, one per SIMD, each a short branch-free loop:
-//   wave 0 (chain)  per sample t: one LDS read per entry (head: W[j]; corrected tail: the earlier
-//                   row's slot; else the gathered value), dot + wave reduction + coefficient, one
-//                   LDS write per entry, the gathers of row t + SK and the row's tail stores
-//                   (fixed 2 + 2 VMEM instructions: s_waitcnt vmcnt(4 SK) finds row t's gather);
-//                   the next sample's slot data is read under the current sample's LDS latency;
+//   * tail entries: gathered from HBM SK + 1 rows ahead by the tail wave into the row's LDS slot,
+//     and corrected: a per-feature tag table over the tail (2 B per tail feature: (row & 255) << 8
+//     | entry of the latest row holding the feature) names the latest of the SK preceding rows
+//     with the same feature, whose new value the chain left in that row's slot in place of x_j;
+//     such entries read that value and are not gathered. Tags never alias: the tagger sweeps
+//     1/128 of the table per row and clears tags older than SK rows, so no tag outlives 256 rows.
+// Four waves, one per SIMD, each a short branch-free loop (two when every feature is in LDS):
+//   wave 0 (chain)  per sample t: one LDS read per entry at the address the tail wave (or the
+//                   loader) wrote, dot + wave reduction + coefficient, one LDS write per entry;
+//                   no VMEM at all -- the next sample's slot data is read under this one's latency;
 //   wave 1 (loader) the partition's CSR entries into an SR-slot LDS ring (16 rows of loads in
 //                   flight in registers, 8-row groups), labels / steps / nnz into a 128-row meta
 //                   ring, 64 rows per batch;
-//   wave 2 (tagger) per row: sweep a tag chunk, tail tag lookups + updates, and each entry's LDS
-//                   read/write addresses (rw) into the slot.
-// Rows are published through LDS counters: loaded (loader), tagged (tagger), done (chain).
+//   wave 2 (tagger) per row: sweep a tag chunk, the tail entries' tag lookups + updates (the raw
+//                   tags into the slot);
+//   wave 3 (tail)   per row: the row's tail stores once the chain has its new values, a later
+//                   row's LDS read / write addresses and its uncorrected tail gathers, an earlier
+//                   row's gathered values into its slot.
+// Rows are published through LDS counters: loaded (loader), tagged (tagger), ready (tail wave),
+// done (chain), stored (tail wave).
 // No MFMA: the work per sample is a ~100-long gather-dot and scatter.
 #include "psgd_device.h"
 
+#include <stddef.h>
 #include <stdlib.h>
 
 namespace psgd {
 
 constexpr int LCAP = 128;                  // entries per row (two per lane)
-#ifndef PSGD_LDS_EXP
-#define PSGD_LDS_EXP 0                     // cost probes (tools/r03_c4_probe.sh); 0 in the product
-#endif
 
 // The chain's tail gathers and stores are buffer instructions over its fp32 vector: a 32-bit
 // byte offset per lane, and lanes without a tail entry get an out-of-range offset, which the
@@ -88,24 +88,40 @@ constexpr int kMetaRing = 128;             // rows of label / step / nnz
 constexpr int kSweepRows = 128;            // the tag table is swept once per this many rows
 constexpr int64_t kLdsCap = 160 * 1024;    // LDS per CU (gfx950)
 
+// The ring of row slots (entries, addresses, gathered tail weights): row u's slot is reused for
+// row u + SR once the chain has read row u (the tail wave and the tagger are done with a row
+// before the chain may run it). The tail wave prepares row i + SK + 1 while the chain is at row
+// i + 1: SR > SK + 2 plus the loader's slack.
+// The ring of new tail weights (the chain's writes of a row's tail entries, read by the SK rows
+// after it as corrections and by the tail wave for the row's stores): row t's entry is rewritten
+// by row t + NVR once the tail wave has issued row t's stores (NVR > SK).
 template <int SK>
 struct LdsRing {
-    // the chain needs rows up to t + SK + 1 staged at sample t (done = t); the loader reuses the
-    // slot of row u - SR once the chain is done with row u - SR + SK (its new values are read by
-    // the SK rows after it): progress needs t + SK + 1 - SR + SK + 1 <= t
-    static constexpr int SR = 2 * SK + 8 <= 16 ? 16 : 32;
-    static_assert(SR >= 2 * SK + 2, "ring too small for the speculation depth");
+    static constexpr int SR = 16;
+    static constexpr int NVR = 16;
+    static_assert(SR >= SK + 6 && NVR > SK, "rings too small for the speculation depth");
 };
 
 struct LdsHeader {
     unsigned loaded;   // rows whose entries are in their slots (loader)
-    unsigned tagged;   // rows whose LDS addresses are in their slots (tagger)
+    unsigned tagged;   // rows whose raw tail tags are in their slots (tagger)
+    unsigned ready;    // rows the chain may run: LDS addresses and gathered tail weights in their
+                       // slots (tail wave; the loader when every feature is in LDS)
     unsigned done;     // rows finished by the chain
-    unsigned stop;
-    unsigned dummy;    // target of inactive lanes' LDS weight reads and writes
+    unsigned stored;   // rows whose tail stores the tail wave has issued (their new-weight ring
+                       // entries may be rewritten); kStoredAll: all landed
+    unsigned stop;     // set by a watchdog only (normal completion needs no stop)
     unsigned dtag;     // target of inactive lanes' tag reads and writes
-    unsigned pad[2];
+    unsigned pad0;
+    unsigned zero[2];  // read by inactive entries: always 0 (never written)
+    unsigned dummy[2]; // written by inactive entries
+    unsigned pad[4];
 };
+constexpr unsigned kLdsZero = 8;           // dword index of LdsHeader::zero (8-byte aligned)
+constexpr unsigned kLdsDummy = 10;         // dword index of LdsHeader::dummy (8-byte aligned)
+constexpr unsigned kStoredAll = 0x7FFFFFFFu;
+static_assert(sizeof(LdsHeader) == 64, "header layout");
+
 template <typename T>
 struct LdsMeta {
     T y[kMetaRing];
@@ -113,91 +129,117 @@ struct LdsMeta {
     double s64[kMetaRing];    // the same in f64 (SquaredL2's alpha)
     int32_t nnz[kMetaRing];
 };
-template <typename T>
+template <typename T, bool TAIL>
 struct LdsSlot {
-    int32_t col[LCAP];   // feature index
-    T val[LCAP];         // x_j; the chain replaces a tail entry's x_j by its new weight
-    uint32_t rw[LCAP];   // LDS dword addresses: read (bits 0-15), write (bits 16-31)
+    int32_t col[LCAP];   // feature index; fp32: the tail wave's gathered weights of the tail entries
+                         // without correction replace it (nobody reads a row's columns after the
+                         // tail wave has prepared it)
+    T val[LCAP];         // x_j
+    uint32_t rw[LCAP];   // the tagger's raw tag of a tail entry's feature, then LDS dword
+                         // addresses: read (bits 0-15) | write (bits 16-31)
+    T g[TAIL && sizeof(T) == 8 ? LCAP : 16 / sizeof(T)];   // fp64: the gathered weights (8 B each)
 };
-// dword index of the target of inactive entries' weight reads and writes (LdsHeader::dummy; an
-// 8-byte aligned pair, pad[0..1], for doubles)
+// the new tail weights of NVR rows
 template <typename T>
-constexpr unsigned lds_dummy() { return sizeof(T) == 8 ? 6 : 4; }
+struct LdsNv {
+    T nv[LCAP];
+};
 constexpr int64_t kMetaOff = sizeof(LdsHeader);
 template <typename T>
 constexpr int64_t slot_off() { return kMetaOff + (int64_t)sizeof(LdsMeta<T>); }
-static_assert(slot_off<float>() % 16 == 0 && sizeof(LdsSlot<float>) % 16 == 0, "alignment");
-static_assert(slot_off<double>() % 16 == 0 && sizeof(LdsSlot<double>) % 16 == 0, "alignment");
+static_assert(slot_off<float>() % 16 == 0 && sizeof(LdsSlot<float, true>) % 16 == 0, "alignment");
+static_assert(slot_off<double>() % 16 == 0 && sizeof(LdsSlot<double, true>) % 16 == 0, "alignment");
 
-template <int SK, typename T>
-constexpr int64_t lds_fixed_bytes() { return slot_off<T>() + LdsRing<SK>::SR * (int64_t)sizeof(LdsSlot<T>); }
+template <int SK, typename T, bool TAIL>
+constexpr int64_t nv_off() { return slot_off<T>() + LdsRing<SK>::SR * (int64_t)sizeof(LdsSlot<T, TAIL>); }
+template <int SK, typename T, bool TAIL>
+constexpr int64_t lds_fixed_bytes() {
+    return (nv_off<SK, T, TAIL>() + (TAIL ? LdsRing<SK>::NVR * (int64_t)sizeof(LdsNv<T>) : 0) + 15) / 16 * 16;
+}
 // tail tag table entries (u16), rounded for the sweep's 4-tag accesses
 __host__ __device__ inline int64_t tag_entries(int64_t d, int64_t K) { return ((d - K) + 3) & ~int64_t(3); }
 template <int SK, typename T>
 int64_t lds_bytes(int64_t d, int64_t K) {
-    return lds_fixed_bytes<SK, T>() + (int64_t)sizeof(T) * K + 2 * tag_entries(d, K);
+    if (K >= d) return lds_fixed_bytes<SK, T, false>() + (int64_t)sizeof(T) * d;
+    return lds_fixed_bytes<SK, T, true>() + (int64_t)sizeof(T) * K + 2 * tag_entries(d, K);
 }
 // Features [0, K) in LDS: all of them when they fit, else as many as leave room for the tail's
 // tag table (K a multiple of 4: the table stays 8-byte aligned); -1 when not even the table fits.
 template <int SK, typename T>
 int64_t lds_head(int64_t d) {
-    const int64_t budget = kLdsCap - lds_fixed_bytes<SK, T>();
-    if ((int64_t)sizeof(T) * d <= budget) return d;
+    if ((int64_t)sizeof(T) * d <= kLdsCap - lds_fixed_bytes<SK, T, false>()) return d;
+    const int64_t budget = kLdsCap - lds_fixed_bytes<SK, T, true>();
     int64_t K = (budget - 2 * (d + 4)) / ((int64_t)sizeof(T) - 2);
     K &= ~int64_t(3);
     return K >= 0 ? K : -1;
 }
 
-// TAIL = false: every feature is in LDS (K = d), the chain issues no VMEM at all.
+// TAIL = false: every feature is in LDS (K = d); two waves (chain, loader), no VMEM on the chain.
+// TAIL = true: features [K, d) in HBM; four waves: chain, loader, tagger, tail. The chain wave
+// issues no VMEM either way: every weight it reads is in LDS (the head, an earlier row's new value,
+// or a tail weight the tail wave gathered into the row's slot).
 // T: the weights' and the arithmetic's type (float: the fp32 throughput mode; double: fp64).
 template <typename S, typename T, int GRAD, int UPD, int SK, bool TAIL>
-__global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams kp, int K) {
+__global__ __launch_bounds__(TAIL ? 256 : 128) void chain_sparse_lds(ChainLaunch L, KParams kp, int K) {
     constexpr bool L2 = UPD == U_SQUARED_L2;
     constexpr bool F64 = sizeof(T) == 8;
     constexpr int SR = LdsRing<SK>::SR;
+    constexpr int NVR = LdsRing<SK>::NVR;
     constexpr unsigned WD = sizeof(T) / 4;                       // dwords per weight
-    constexpr unsigned kLdsDummy = lds_dummy<T>();
     constexpr int64_t kSlotOff = slot_off<T>();
+    using Slot = LdsSlot<T, TAIL>;
     static_assert((SR & (SR - 1)) == 0, "slot index by mask");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     LdsHeader* hdr = reinterpret_cast<LdsHeader*>(smem);
     LdsMeta<T>* meta = reinterpret_cast<LdsMeta<T>*>(smem + kMetaOff);
-    LdsSlot<T>* slots = reinterpret_cast<LdsSlot<T>*>(smem + kSlotOff);
+    Slot* slots = reinterpret_cast<Slot*>(smem + kSlotOff);
     float* lds = reinterpret_cast<float*>(smem);                 // dword-addressed view
     // a weight (or a slot's value) at dword index i
     auto ld_w = [&](unsigned i) __attribute__((always_inline)) -> T { return *reinterpret_cast<const T*>(lds + i); };
     auto st_w = [&](unsigned i, T v) __attribute__((always_inline)) { *reinterpret_cast<T*>(lds + i) = v; };
-    constexpr unsigned kWoff = (unsigned)(lds_fixed_bytes<SK, T>() / 4);
+    constexpr unsigned kWoff = (unsigned)(lds_fixed_bytes<SK, T, TAIL>() / 4);
     T* W = reinterpret_cast<T*>(lds + kWoff);                    // head weights [K]
     uint16_t* tagpos = reinterpret_cast<uint16_t*>(W + K);       // tail features K .. d-1
-    // dword index of val[0] of the slot holding row u
-    auto val_off = [](int32_t u) __attribute__((always_inline)) -> unsigned {
-        return (unsigned)((kSlotOff + (int64_t)(u & (SR - 1)) * (int64_t)sizeof(LdsSlot<T>)) / 4) + LCAP;
+    // dword index of val[0] / g[0] of the slot holding row u
+    auto slot_dw = [](int32_t u) __attribute__((always_inline)) -> unsigned {
+        return (unsigned)((kSlotOff + (int64_t)(u & (SR - 1)) * (int64_t)sizeof(Slot)) / 4);
     };
+    // gathered tail weights: fp32 in place of the row's columns, fp64 in g
+    constexpr unsigned kGDw = (unsigned)((F64 ? offsetof(Slot, g) : offsetof(Slot, col)) / 4);
+    // dword index of nv[0] of the new-weight ring entry of row t
+    auto nv_dw = [](int32_t t) __attribute__((always_inline)) -> unsigned {
+        return (unsigned)((nv_off<SK, T, TAIL>() + (int64_t)(t & (NVR - 1)) * (int64_t)sizeof(LdsNv<T>)) / 4);
+    };
+    LdsNv<T>* nvring = reinterpret_cast<LdsNv<T>*>(smem + nv_off<SK, T, TAIL>());
+    // K's bit 30 (PSGD_LDS_PROBE=1, diagnostics only): the tail wave's stores and gathers touch no
+    // memory (wrong results; measures what the tail's memory traffic costs)
+    const bool probe = ((K >> 30) & 1) != 0;
+    K &= 0x3FFFFFFF;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int chain = blockIdx.x;
     const ChainDesc dsc = L.descs[chain];
     const int d = kp.d;
-    // row indices run in 32-bit: a chain's rows (>= 16 B each with the label) live in HBM, so
-    // n < 2^31; the CSR offsets stay 64-bit (the loader's row_ptr values)
+    // row indices run in 32-bit (the host runs this kernel only for n <= INT32_MAX); the CSR
+    // offsets stay 64-bit (the loader's row_ptr values)
     const int32_t n = (int32_t)dsc.n_rows;
-    const int32_t NT = (int32_t)tag_entries(d, K);
-    // The chain runs n_pad samples (a multiple of its unroll SK + 1) and reads up to row
-    // n_pad + SK ahead: the loader and the tagger stage n_fill rows, rows past n null (no
-    // entries, label and step 0), so no read in the chain needs a condition.
-    constexpr int GS = SK + 1;
+    const int32_t NT = TAIL ? (int32_t)tag_entries(d, K) : 0;
+    // The chain runs n_pad samples (a multiple of its unroll) and reads row t + 1 at sample t:
+    // the other waves stage n_fill rows, rows past n null (no entries, label and step 0), so no
+    // read in the chain needs a condition.
+    constexpr int GS = 2;
     const int32_t n_pad = (n + GS - 1) / GS * GS;
-    const int32_t n_fill = (n_pad + SK + 1 + 7) / 8 * 8;
-    // [d] (tail used) + [128] the loader's dummy sources + [1024] the chain's dummy targets (in
-    // T: for doubles the chain's slice of L.wf32 is twice as long, launch_sparse_lds64_chains)
+    const int32_t n_fill = (n_pad + 1 + 7) / 8 * 8;
+    // [d] (tail used) + [128] the loader's dummy sources + [1024] spare (in T: for doubles the
+    // chain's slice of L.wf32 is twice as long, launch_sparse_lds64_chains)
     T* V = reinterpret_cast<T*>(L.wf32 + (int64_t)chain * L.wstride);
+    constexpr unsigned kShift = F64 ? 3 : 2;
 
     for (int32_t i = threadIdx.x; i < NT; i += blockDim.x) tagpos[i] = 0xFFFF;
     for (int i = threadIdx.x; i < K; i += blockDim.x) W[i] = T(as_global(L.w_in)[i]);
-    if (threadIdx.x < 8) reinterpret_cast<unsigned*>(hdr)[threadIdx.x] = 0;
+    if (threadIdx.x < 16) reinterpret_cast<unsigned*>(hdr)[threadIdx.x] = 0;
     if constexpr (F64 && TAIL) {
-        // the tail V[K, d) starts as w_in; the chain's gathers (sc1, through L2) must see it
+        // the tail V[K, d) starts as w_in; the tail wave's gathers (sc1, through L2) must see it
         for (int i = K + threadIdx.x; i < d; i += blockDim.x) V[i] = as_global(L.w_in)[i];
         __threadfence();
     }
@@ -206,7 +248,8 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
 
     uint64_t st_wait = 0;                     // diagnostic (PSGD_STAMPS): cycles spent waiting
     const uint64_t st_begin = __builtin_amdgcn_s_memtime();
-    // wait until *flag >= need (cached in `seen`); false when the chain stopped or the watchdog fired
+    // wait until *flag >= need (cached in `seen`); false when the watchdog fired (here or in
+    // another wave)
     auto wait_for = [&](unsigned& seen, const unsigned* flag, int32_t need, int code)
         __attribute__((always_inline)) -> bool {
         if ((int32_t)seen >= need) return true;
@@ -242,8 +285,8 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
     };
     auto stamp_out = [&](int k) __attribute__((always_inline)) {
         if (L.stamps && lane == 0) {
-            L.stamps[(size_t)chain * 6 + 2 * k] = __builtin_amdgcn_s_memtime() - st_begin;
-            L.stamps[(size_t)chain * 6 + 2 * k + 1] = st_wait;
+            L.stamps[(size_t)chain * 16 + 2 * k] = __builtin_amdgcn_s_memtime() - st_begin;
+            L.stamps[(size_t)chain * 16 + 2 * k + 1] = st_wait;
         }
     };
 
@@ -294,29 +337,28 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
                 G.ic[q] = ic;
             }
         };
-        // rows u0 .. u0 + 7 (those < n_fill) into their slots, each once the chain is done with the
-        // row its slot held (row u - SR, read by the chain up to row u - SR + SK), published row
-        // by row: the chain at sample t waits for row t + SK + 1
+        // rows u0 .. u0 + 7 (those < n_fill) into their slots, each once its slot's previous row
+        // u - SR is released (the chain has read it), published row by row
         auto stage_group = [&](int32_t u0, const Group& G) __attribute__((always_inline)) -> bool {
             bool good = true;
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 const int32_t u = u0 + q;
                 if (good && u < n_fill) {
-                    good = wait_for(done, &hdr->done, u - SR + SK + 1, 16);
-                    LdsSlot<T>& sl = slots[u & (SR - 1)];
+                    good = wait_for(done, &hdr->done, u - SR + 1, 16);
+                    Slot& sl = slots[u & (SR - 1)];
                     sl.col[lane] = G.ca[q];
                     sl.col[lane + 64] = G.cb[q];
                     sl.val[lane] = G.ia[q] ? T(G.xa[q]) : T(0);
                     sl.val[lane + 64] = G.ic[q] ? T(G.xb[q]) : T(0);
                     if constexpr (!TAIL) {
-                        // every feature in LDS: the entry's read and write address is W[j]
-                        // (no tagger); inactive entries have x = 0 and use the dummy dword
-                        const unsigned ha = G.ia[q] ? kWoff + WD * (unsigned)G.ca[q] : kLdsDummy;
-                        const unsigned hb = G.ic[q] ? kWoff + WD * (unsigned)G.cb[q] : kLdsDummy;
-                        sl.rw[lane] = ha | (ha << 16);
-                        sl.rw[lane + 64] = hb | (hb << 16);
-                        publish(&hdr->tagged, u + 1);
+                        // every feature in LDS: the entry's read and write address is W[j] (no
+                        // tagger, no tail wave); inactive entries read the zero pair and write
+                        // the dummy pair
+                        const unsigned ha = kWoff + WD * (unsigned)G.ca[q], hb = kWoff + WD * (unsigned)G.cb[q];
+                        sl.rw[lane] = G.ia[q] ? ha | (ha << 16) : kLdsZero | (kLdsDummy << 16);
+                        sl.rw[lane + 64] = G.ic[q] ? hb | (hb << 16) : kLdsZero | (kLdsDummy << 16);
+                        publish(&hdr->ready, u + 1);
                     }
                     publish(&hdr->loaded, u + 1);
                 }
@@ -355,27 +397,28 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
         return;
     }
 
-    if (wave == 2 && !TAIL) return;   // the loader writes the addresses
+    if constexpr (TAIL) {
     if (wave == 2) {
-        // ---------------- tagger: tail tags and each entry's LDS read / write address ----------
-        // Four rows per step, so that their LDS round trips overlap: the rows' columns, then the
-        // sweeps, then each row's tag lookups and updates in row order (one wave's LDS operations
-        // execute in program order, so row u+1's lookups see row u's updates), then the rows'
-        // addresses.
+        // ---------------- tagger: the tail features' latest rows ----------------
+        // Per row, for each tail entry, the tag of its feature -- (row & 255) << 8 | entry of the
+        // latest row that held it -- is read (into the slot's rw word, for the tail wave) and
+        // replaced by this row's. Four rows per step, so that their LDS round trips overlap: the
+        // rows' columns, then the sweeps, then each row's lookups and updates in row order (one
+        // wave's LDS operations execute in program order, so row u+1's lookups see row u's
+        // updates), then the raw tags into the slots.
         constexpr int TB = 4;
         unsigned loaded = 0;
         uint16_t* dtag = reinterpret_cast<uint16_t*>(&hdr->dtag);
         const int32_t chunk = ((NT + kSweepRows - 1) / kSweepRows + 255) & ~int32_t(255);
         static_assert(8 % TB == 0, "n_fill is a multiple of TB");
         for (int32_t u0 = 0; u0 < n_fill; u0 += TB) {
-            constexpr int nb = TB;
-            if (!wait_for(loaded, &hdr->loaded, u0 + nb, 32)) break;
+            if (!wait_for(loaded, &hdr->loaded, u0 + TB, 32)) break;
             int nnz[TB];
             int32_t ca[TB], cb[TB];
 #pragma unroll
             for (int q = 0; q < TB; ++q) {
                 const int32_t u = u0 + q;
-                const LdsSlot<T>& sl = slots[u & (SR - 1)];
+                const Slot& sl = slots[u & (SR - 1)];
                 nnz[q] = meta->nnz[u & (kMetaRing - 1)];
                 ca[q] = sl.col[lane];
                 cb[q] = sl.col[lane + 64];
@@ -412,14 +455,14 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
                     if (sok[q]) *reinterpret_cast<uint64_t*>(tagpos + si[q]) = sweep4(sv[q]);
             } else {
 #pragma unroll
-            for (int q = 0; q < TB; ++q) {
-                const int32_t lo = ((u0 + q) & (kSweepRows - 1)) * chunk;
-                const int32_t hi = lo + chunk < NT ? lo + chunk : NT;
-                for (int32_t i = lo + 4 * lane; i < hi; i += 256) {
-                    const uint64_t v = *reinterpret_cast<const uint64_t*>(tagpos + i);
-                    *reinterpret_cast<uint64_t*>(tagpos + i) = sweep4(v);
+                for (int q = 0; q < TB; ++q) {
+                    const int32_t lo = ((u0 + q) & (kSweepRows - 1)) * chunk;
+                    const int32_t hi = lo + chunk < NT ? lo + chunk : NT;
+                    for (int32_t i = lo + 4 * lane; i < hi; i += 256) {
+                        const uint64_t v = *reinterpret_cast<const uint64_t*>(tagpos + i);
+                        *reinterpret_cast<uint64_t*>(tagpos + i) = sweep4(v);
+                    }
                 }
-            }
             }
             unsigned va[TB], vb[TB];
 #pragma unroll
@@ -436,136 +479,191 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
             }
 #pragma unroll
             for (int q = 0; q < TB; ++q) {
-                const int32_t u = u0 + q;
-                auto rw_of = [&](int e, int32_t c, unsigned v) __attribute__((always_inline)) -> uint32_t {
-                    const bool tail = c >= K;
-                    const unsigned dl = ((unsigned)u - (v >> 8)) & 255;
-                    const bool prev = v != 0xFFFF && dl >= 1 && dl <= SK;
-                    const unsigned rd_tail = prev ? val_off(u - dl) + WD * (v & 255) : kLdsDummy;
-                    const unsigned wr_tail = val_off(u) + WD * (unsigned)e;
-                    const unsigned head = kWoff + WD * (unsigned)c;
-                    const unsigned rd = e >= nnz[q] ? kLdsDummy : tail ? rd_tail : head;
-                    const unsigned wr = e >= nnz[q] ? kLdsDummy : tail ? wr_tail : head;
-                    return rd | (wr << 16);
-                };
-                if (q < nb) {
-                    LdsSlot<T>& sl = slots[u & (SR - 1)];
-                    sl.rw[lane] = rw_of(lane, ca[q], va[q]);
-                    sl.rw[lane + 64] = rw_of(lane + 64, cb[q], vb[q]);
-                }
+                Slot& sl = slots[(u0 + q) & (SR - 1)];
+                sl.rw[lane] = va[q];
+                sl.rw[lane + 64] = vb[q];
             }
-            publish(&hdr->tagged, u0 + nb);
+            publish(&hdr->tagged, u0 + TB);
         }
         stamp_out(2);
         return;
     }
 
+    if (wave == 3) {
+        // ---------------- tail wave: the tail's HBM traffic, off the chain ----------------
+        // Iteration i (one per row, i from -A):
+        //   1. row i + 3's gathered weights into its slot (issued WB iterations ago), publish
+        //      `ready` (the chain at row t needs row t + 1); first, so that the chain never waits
+        //      behind this iteration's wait for it;
+        //   2. row i's new tail weights (the chain's writes into the new-weight ring) once the
+        //      chain is done with row i;
+        //   3. row u = i + A's LDS addresses from its raw tags, row i's tail stores, and the
+        //      gathers of row u's tail entries that no row in u - SK .. u - 1 corrects. The gather
+        //      follows this wave's stores of rows <= u - SK - 1 in program order, so L2 serves it
+        //      after them (sc1 loads); rows u - SK .. u - 1 are the correction window (their new
+        //      values, in LDS).
+        // Each iteration issues exactly 2 + 2 VMEM instructions (no-access offsets where there is
+        // nothing to move), so the vmcnt of step 1 is a constant.
+        constexpr int A = SK + 1;
+        constexpr int WB = A - 3;   // iterations a gather has to land
+        static_assert(WB >= 2, "speculation depth too small for the tail wave's pipeline");
+        const i32x4 vrs = buffer_rsrc(reinterpret_cast<const float*>(V), (uint32_t)((int64_t)d * sizeof(T)));
+        unsigned done = 0, tagged = 0;
+        bool ok = true;
+        T gr[A][2];
+        uint32_t so[A][2];
+#pragma unroll
+        for (int q = 0; q < A; ++q) so[q][0] = so[q][1] = kNoAccess;
+        // The slot data of row u that its addresses and gathers need, read one iteration ahead
+        // (unconditionally, past a spin-only branch: rows past n_fill read a live slot and count
+        // as empty).
+        struct Pre { int nz; int32_t c[2]; unsigned v[2]; };
+        auto pre_read = [&](int32_t u) __attribute__((always_inline)) -> Pre {
+            if (u < n_fill && (int32_t)tagged < u + 1) ok = ok && wait_for(tagged, &hdr->tagged, u + 1, 256);
+            const Slot& sl = slots[u & (SR - 1)];
+            return Pre{meta->nnz[u & (kMetaRing - 1)], {sl.col[lane], sl.col[lane + 64]}, {sl.rw[lane], sl.rw[lane + 64]}};
+        };
+        // row u's read / write addresses into its slot; its gather and store offsets
+        // Branch-free (selects on 32-bit values, the row's constants uniform).
+        auto prepare = [&](int32_t u, const Pre& P, uint32_t (&go)[2], uint32_t (&sv)[2]) __attribute__((always_inline)) {
+            const int nz = u < n_fill ? P.nz : 0;
+            const unsigned gb = slot_dw(u) + kGDw;            // this row's gathered weights
+            const unsigned wb = nv_dw(u);                      // this row's new-weight entry
+            constexpr unsigned kNvW = (unsigned)(sizeof(LdsNv<T>) / 4);
+            constexpr unsigned kNv0 = (unsigned)(nv_off<SK, T, TAIL>() / 4);
+            unsigned rwv[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const unsigned e = (unsigned)(lane + 64 * h);
+                const unsigned c = (unsigned)P.c[h], v = P.v[h];
+                const unsigned dl = ((unsigned)u - (v >> 8)) & 255;
+                const bool prev = (v != 0xFFFFu) & (dl - 1u < (unsigned)SK);
+                const bool act = e < (unsigned)nz, tail = c >= (unsigned)K;
+                const unsigned head = kWoff + WD * c;
+                const unsigned nvp = kNv0 + (((unsigned)u - dl) & (NVR - 1)) * kNvW + WD * (v & 255);
+                const unsigned rt = prev ? nvp : gb + WD * e;
+                const unsigned rd = act ? (tail ? rt : head) : kLdsZero;
+                const unsigned wr = act ? (tail ? wb + WD * e : head) : kLdsDummy;
+                const unsigned off = probe ? kNoAccess : c << kShift;
+                const bool at = act & tail;
+                sv[h] = at ? off : kNoAccess;
+                go[h] = (at & !prev) ? off : kNoAccess;
+                rwv[h] = rd | (wr << 16);
+            }
+            if (u < n_fill) {
+                Slot& sl = slots[u & (SR - 1)];
+                sl.rw[lane] = rwv[0];
+                sl.rw[lane + 64] = rwv[1];
+            }
+        };
+        Pre pre = pre_read(0);
+        // PSGD_STAMPS: cycles of the iteration's phases (vmcnt wait of step 1, the new-weight read
+        // before the stores, prepare + VMEM issue, the next row's prefetch)
+        uint64_t ph[4] = {0, 0, 0, 0};
+        auto tick = [&](int k, uint64_t& m) __attribute__((always_inline)) {
+            if (L.stamps) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                const uint64_t now = __builtin_amdgcn_s_memtime();
+                ph[k] += now - m;
+                m = now;
+            }
+        };
+        auto iteration = [&](auto qc, int32_t i) __attribute__((always_inline)) {
+            uint64_t mark = L.stamps ? __builtin_amdgcn_s_memtime() : 0;
+            constexpr int Q = decltype(qc)::value;            // i mod A (rows i and i + A)
+            constexpr int QW = (Q + 3) % A;                   // (i + 3) mod A
+            // 1. row i + 3's gathered weights into its slot, publish it: first, so that the
+            //    chain's next rows never wait behind this iteration's wait for the chain. They were
+            //    issued at iteration i + 3 - A; 4 (WB - 1) VMEM instructions came after them.
+            const int32_t r = i + 3;
+            if (r >= 0 && r < n_fill) {
+                asm volatile("s_waitcnt vmcnt(%2)" : "+v"(gr[QW][0]), "+v"(gr[QW][1]) : "i"(4 * (WB - 1)) : "memory");
+                tick(0, mark);
+                T* gdst = reinterpret_cast<T*>(lds + slot_dw(r) + kGDw);
+                gdst[lane] = gr[QW][0];
+                gdst[lane + 64] = gr[QW][1];
+                publish(&hdr->ready, r + 1);
+            }
+            // 2. row i's new tail weights, once the chain has them (read unconditionally: rows
+            //    before 0 have no-access store offsets)
+            if (i >= 0 && i < n_pad && (int32_t)done < i + 1) ok = ok && wait_for(done, &hdr->done, i + 1, 128);
+            const LdsNv<T>& nr = nvring[i & (NVR - 1)];
+            const T nv0 = nr.nv[lane], nv1 = nr.nv[lane + 64];
+            if (L.stamps) { tick(3, mark); asm volatile("" : : "v"(nv0), "v"(nv1)); tick(1, mark); }
+            // 3. row u = i + A's addresses and offsets (under the read above), then row i's
+            //    stores and row u's gathers, in that order (the gathers must follow the stores of
+            //    rows <= u - SK - 1 = i)
+            const int32_t u = i + A;
+            uint32_t go[2];
+            const uint32_t s0 = so[Q][0], s1 = so[Q][1];
+            prepare(u, pre, go, so[Q]);
+            buffer_store_f32(vrs, s0, nv0);
+            buffer_store_f32(vrs, s1, nv1);
+            gr[Q][0] = buffer_gather_sc1(vrs, go[0], T(0));
+            gr[Q][1] = buffer_gather_sc1(vrs, go[1], T(0));
+            if (i >= 0) publish(&hdr->stored, i + 1);
+            tick(2, mark);
+            // the next row's slot data, in flight under the next iteration's first steps
+            pre = pre_read(u + 1);
+            tick(3, mark);
+        };
+        for (int32_t i0 = -A; ok && i0 < n_fill; i0 += A)
+            static_for<A>([&](auto qc) {
+                const int32_t i = i0 + decltype(qc)::value;
+                if (ok && i < n_fill) iteration(qc, i);
+            });
+        // every store has landed before the chain reads the tail back (fp64) or the kernel ends
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int q = 0; q < A; ++q) asm volatile("" : : "v"(gr[q][0]), "v"(gr[q][1]));
+        if (ok) publish(&hdr->stored, (int32_t)kStoredAll);
+        stamp_out(3);
+        if (L.stamps && lane == 0)
+            for (int k = 0; k < 4; ++k) L.stamps[(size_t)chain * 16 + 8 + k] = ph[k];
+        return;
+    }
+    }   // TAIL
+
     // ---------------- chain ----------------
-    // The per-sample code is straight-line: the flag checks come before the LDS reads they
-    // guard and branch only to a spin, so no read result crosses a branch (a join would make
-    // the compiler wait for it). The loop runs a multiple of SK + 1 samples; samples past n are
-    // null (no entries, LDS traffic to the dummy dword, no loss), so every gather's registers
-    // have a consumer: the compiler treats an asm load's result as written at issue, and a dead
-    // one's registers could be reused while the load is still in flight.
+    // Only LDS: per sample, one read per entry at its read address (head W[j]; an earlier row's
+    // new value; the gathered tail weight; the zero pair), the dot, wave reduction and
+    // coefficient, one write per entry at its write address (head W[j]; the slot, for the tail
+    // wave's store and later rows' corrections; the dummy pair). Straight-line: the flag check
+    // branches only to a spin, so no read result crosses a branch (a join would make the compiler
+    // wait for it). Samples past n are null (no entries, no loss).
     double alpha = 1.0;       // SquaredL2: w = alpha * v
     double dnsq = 0.0;        // SquaredL2, fp32: ||v||^2 - ||v_0||^2 (this lane)
     double loss_sum = 0.0;
     float loss_blk = 0.0f;
     int64_t count = 0;
-    unsigned loaded = 0, tagged = 0;
-    constexpr unsigned kShift = F64 ? 3 : 2;
-    const i32x4 vrs = buffer_rsrc(reinterpret_cast<const float*>(V), (uint32_t)((int64_t)d * sizeof(T)));   // [0, d)
-    auto boff = [](bool on, int32_t c) __attribute__((always_inline)) -> uint32_t {
-        return on ? (uint32_t)c << kShift : kNoAccess;
-    };
-    // gathered tail weights: row u's in gr[u % (SK + 1)]. A gather's registers are written by
-    // the load when it lands, so they are never copied before their s_waitcnt: the gather of
-    // row t + SK goes to the set row t - 1 used, and the loop is unrolled SK + 1 times
-    T gr[GS][2];
+    unsigned ready = 0, stored = 0;
     bool ok = true;
-    // wait until rows < nl are loaded and rows < nt tagged (the spin path only)
-    auto need = [&](int32_t nl, int32_t nt) __attribute__((always_inline)) {
-        nl = nl < n_fill ? nl : n_fill;
-        nt = nt < n_fill ? nt : n_fill;
-        if ((int32_t)loaded < nl || (int32_t)tagged < nt) {
-            ok = ok && wait_for(loaded, &hdr->loaded, nl, 2);
-            ok = ok && wait_for(tagged, &hdr->tagged, nt, 4);
-        }
-    };
-    // the entries of row u a gather needs
-    struct GCols { int32_t c0, c1; int nnz; };
-    auto gcols = [&](int32_t u) __attribute__((always_inline)) -> GCols {
-        const LdsSlot<T>& sl = slots[u & (SR - 1)];
-        const int nz = meta->nnz[u & (kMetaRing - 1)];
-        return GCols{sl.col[lane], sl.col[lane + 64], nz};
-    };
-    // Only tail entries touch memory: the other lanes get the no-access offset.
-    auto gather = [&](const GCols& G, T (&g)[2]) __attribute__((always_inline)) {
-#if PSGD_LDS_EXP & 2   // experiment: the tail gathers read nothing (wrong results; cost probe)
-        const bool a0 = false, a1 = false;
-#else
-        const bool a0 = lane < G.nnz && G.c0 >= K, a1 = lane + 64 < G.nnz && G.c1 >= K;
-#endif
-        g[0] = buffer_gather_sc1(vrs, boff(a0, G.c0), T(0));
-        g[1] = buffer_gather_sc1(vrs, boff(a1, G.c1), T(0));
+    // rows < nr ready; with a tail, row t's new-weight ring entry free (row t - NVR stored)
+    auto need = [&](int32_t nr, int32_t t) __attribute__((always_inline)) {
+        nr = nr < n_fill ? nr : n_fill;
+        if ((int32_t)ready < nr) ok = ok && wait_for(ready, &hdr->ready, nr, 2);
+        if constexpr (TAIL)
+            if ((int32_t)stored < t - NVR + 1) ok = ok && wait_for(stored, &hdr->stored, t - NVR + 1, 8);
     };
     // the data of sample t
-    struct Row { T x0, x1; uint32_t rw0, rw1; int32_t c0, c1; int nnz; T y, s; double s64; };
+    struct Row { T x0, x1; uint32_t rw0, rw1; T y, s; double s64; };
     auto row_of = [&](int32_t t) __attribute__((always_inline)) -> Row {
-        const LdsSlot<T>& sl = slots[t & (SR - 1)];
+        const Slot& sl = slots[t & (SR - 1)];
         const int m = (int)(t & (kMetaRing - 1));
-        return Row{sl.val[lane], sl.val[lane + 64], sl.rw[lane], sl.rw[lane + 64], sl.col[lane],
-                   sl.col[lane + 64], meta->nnz[m], meta->y[m], meta->s[m], L2 ? meta->s64[m] : 0.0};
+        return Row{sl.val[lane], sl.val[lane + 64], sl.rw[lane], sl.rw[lane + 64], meta->y[m], meta->s[m],
+                   L2 ? meta->s64[m] : 0.0};
     };
-    // prologue: gathers of rows 0 .. SK-1, each followed by two no-access stores, the same VMEM
-    // pattern as a sample of the loop; then the columns of row SK and the data of sample 0
-    GCols gc{0, 0, 0};
-    if constexpr (TAIL) {
-        static_for<SK>([&](auto qc) {
-            constexpr int q = decltype(qc)::value;
-            need(q + 1, 0);
-            gather(gcols(q), gr[q]);
-            buffer_store_f32(vrs, kNoAccess, T(0));
-            buffer_store_f32(vrs, kNoAccess, T(0));
-        });
-        need(SK + 1, 1);
-        gc = gcols(SK);
-    } else {
-        need(0, 1);
-    }
+    need(1, 0);
     Row cur = row_of(0);
-    auto sample = [&](auto qc, int32_t t) __attribute__((always_inline)) {
-        constexpr int Q = decltype(qc)::value;           // t % GS
-        constexpr int QN = (Q + SK) % GS;                 // (t + SK) % GS
-        // the rows the reads below need (a branch to the spin only)
-        need(TAIL ? t + SK + 2 : 0, t + 2);
-        // this sample's weight reads (after the previous sample's writes, in program order),
-        // row t + SK's gather, then the columns of row t + SK + 1 and the data of sample t + 1:
-        // all issued before anything waits (the scheduling barrier keeps the compiler from
-        // sinking the prefetch below the arithmetic), so their LDS round trips overlap
-        const unsigned r0 = cur.rw0 & 0xFFFF, r1 = cur.rw1 & 0xFFFF;
-        const T l0 = ld_w(r0), l1 = ld_w(r1);
+    auto sample = [&](int32_t t) __attribute__((always_inline)) {
+        need(t + 2, t);
+        // this sample's weight reads (after the previous sample's writes, in program order) and
+        // the data of sample t + 1, issued before anything waits (the scheduling barriers keep
+        // the compiler from sinking the prefetch below the arithmetic)
+        const T w0 = ld_w(cur.rw0 & 0xFFFF), w1 = ld_w(cur.rw1 & 0xFFFF);
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (TAIL) {
-            gather(gc, gr[QN]);
-            gc = gcols(t + SK + 1);
-        }
         const Row nxt = row_of(t + 1);
         __builtin_amdgcn_sched_barrier(0);
-        T w0 = l0, w1 = l1;
-        if constexpr (TAIL) {
-            // row t's gather: issued SK samples ago, followed by 4 SK VMEM instructions
-            // (PSGD_STAMPS: the time this wait takes is the chain's "wait" counter)
-            uint64_t vm0 = 0;
-            if (L.stamps) vm0 = __builtin_amdgcn_s_memtime();
-            asm volatile("s_waitcnt vmcnt(%2)" : "+v"(gr[Q][0]), "+v"(gr[Q][1]) : "i"(4 * SK) : "memory");
-            if (L.stamps) st_wait += __builtin_amdgcn_s_memtime() - vm0;
-            // head: W[j]; tail also in rows t-SK .. t-1: that row's new value; else the gather
-            w0 = r0 == kLdsDummy ? gr[Q][0] : l0;
-            w1 = r1 == kLdsDummy ? gr[Q][1] : l1;
-        }
-        w0 = lane < cur.nnz ? w0 : T(0);
-        w1 = lane + 64 < cur.nnz ? w1 : T(0);
         T acc = cur.x0 * w0;
         acc = m_fma(cur.x1, w1, acc);
         T z = wave_sum_uniform(acc);
@@ -594,35 +692,19 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
         if constexpr (L2 && !F64) dnsq += nsq_delta(w0, nv0) + nsq_delta(w1, nv1);
         st_w(cur.rw0 >> 16, nv0);
         st_w(cur.rw1 >> 16, nv1);
-        // this row's tail stores (2 VMEM instructions)
-        if constexpr (TAIL) {
-            const bool a0 = lane < cur.nnz && cur.c0 >= K, a1 = lane + 64 < cur.nnz && cur.c1 >= K;
-#if PSGD_LDS_EXP & 1   // experiment: the tail stores go nowhere (wrong results; cost probe)
-            buffer_store_f32(vrs, kNoAccess, nv0);
-            buffer_store_f32(vrs, kNoAccess, nv1);
-#else
-            buffer_store_f32(vrs, boff(a0, cur.c0), nv0);
-            buffer_store_f32(vrs, boff(a1, cur.c1), nv1);
-#endif
-        }
         publish(&hdr->done, t + 1);
         cur = nxt;
     };
     for (int32_t t = 0; ok && t < n_pad; t += GS)
-        static_for<GS>([&](auto qc) { sample(qc, t + decltype(qc)::value); });
+        static_for<GS>([&](auto qc) { sample(t + decltype(qc)::value); });
     count = ok ? n : 0;
-    __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // the last gathers' registers stay allocated until they have landed
-#pragma unroll
-    for (int q = 0; q < GS; ++q) asm volatile("" : : "v"(gr[q][0]), "v"(gr[q][1]));
     stamp_out(0);
     loss_sum += double(loss_blk);
     if constexpr (GRAD == G_LEAST_SQUARES && !F64) loss_sum = loss_sum / 2.0;
     if constexpr (F64) {
         // w = alpha v into the chain's row of L.w_out (the f64 fold), regVal of the chain's last
-        // update (PSGD.scala:257) from ||w||: the head from LDS, the tail from V (this wave's
-        // own stores, landed above; read through L2 like its gathers)
+        // update (PSGD.scala:257) from ||w||: the head from LDS, the tail from V once the tail
+        // wave's stores have all landed (read through L2 like its gathers)
         double* wo = L.w_out + (int64_t)chain * d;
         double nsq = 0.0;
         for (int i = lane; i < K; i += 64) {
@@ -631,6 +713,8 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
             if constexpr (L2) nsq += wv * wv;
         }
         if constexpr (TAIL) {
+            ok = ok && wait_for(stored, &hdr->stored, (int32_t)kStoredAll, 2);
+            const i32x4 vrs = buffer_rsrc(reinterpret_cast<const float*>(V), (uint32_t)((int64_t)d * sizeof(T)));
             // 8 loads in flight per lane (out-of-range lanes: the no-access offset, read as 0)
             for (int i0 = K; i0 < d; i0 += 8 * 64) {
                 double vv[8];
@@ -683,7 +767,11 @@ static int lds_upd(const ChainLaunch& L, const KParams& kp, int upd, int K, size
                       : (upd == U_SIMPLE ? chain_sparse_lds<S, T, GRAD, U_SIMPLE, SK, false>
                                          : chain_sparse_lds<S, T, GRAD, U_SQUARED_L2, SK, false>);
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(192), lds, st, L, kp, K);
+    static const bool probe = [] {
+        const char* e = getenv("PSGD_LDS_PROBE");
+        return e && *e == '1';
+    }();
+    hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(K < kp.d ? 256 : 128), lds, st, L, kp, probe ? K | (1 << 30) : K);
     return (int)hipGetLastError();
 }
 
@@ -697,7 +785,7 @@ static int lds_grad(const ChainLaunch& L, const KParams& kp, int grad, int upd, 
     }
 }
 
-// Variant 600 + 10 (SK == 8) + 20 (fp64 compute) + storage (1: f32 rows).
+// Variant 600 + 10 (SK == 4) + 20 (fp64 compute) + storage (1: f32 rows).
 template <int SK, typename T>
 static int lds_launch(const ChainLaunch& L, const KParams& kp, int storage, int gradient, int updater,
                       hipStream_t stream, int* kernel_variant) {
@@ -707,16 +795,17 @@ static int lds_launch(const ChainLaunch& L, const KParams& kp, int storage, int 
     if (const char* e = getenv("PSGD_SPARSE_LDS_HEAD"))
         if (*e) { const int64_t cap = atoll(e) & ~int64_t(3); if (cap >= 0 && cap < K) K = cap; }
     const size_t lds = (size_t)lds_bytes<SK, T>(kp.d, K);
-    if (kernel_variant) *kernel_variant = 600 + (SK == 8 ? 10 : 0) + (sizeof(T) == 8 ? 20 : 0) + storage;
+    if (kernel_variant) *kernel_variant = 600 + (SK == 4 ? 10 : 0) + (sizeof(T) == 8 ? 20 : 0) + storage;
     if (storage == 1) return lds_grad<float, T, SK>(L, kp, gradient, updater, (int)K, lds, stream);
     return lds_grad<double, T, SK>(L, kp, gradient, updater, (int)K, lds, stream);
 }
 
-// Speculation depth: 4 rows by default (tail gathers are L2 hits once the tails fit L2);
-// PSGD_SPARSE_SK=8 for A/B measurements (read at every launch).
+// Speculation depth (the correction window, and the tail wave's gather lead SK + 1, which leaves
+// its gathers SK - 2 rows to land): 8 rows by default; PSGD_SPARSE_SK=4 for A/B measurements and
+// tests (read at every launch).
 static int lds_depth() {
     const char* e = getenv("PSGD_SPARSE_SK");
-    return (e && atoi(e) == 8) ? 8 : 4;
+    return (e && atoi(e) == 4) ? 4 : 8;
 }
 
 // The chain, loader and tagger waves keep row numbers in 32 bits (psgd_sparse_lds.hip: n): a
@@ -724,24 +813,24 @@ static int lds_depth() {
 // chain_sparse / chain_general instead.
 bool sparse_lds_applies(int64_t d, int64_t max_nnz, int64_t n_max) {
     if (max_nnz > LCAP || n_max > (int64_t)INT32_MAX) return false;
-    return (lds_depth() == 8 ? lds_head<8, float>(d) : lds_head<4, float>(d)) >= 0;
+    return (lds_depth() == 4 ? lds_head<4, float>(d) : lds_head<8, float>(d)) >= 0;
 }
 
-int64_t sparse_lds_head(int64_t d) { return lds_depth() == 8 ? lds_head<8, float>(d) : lds_head<4, float>(d); }
+int64_t sparse_lds_head(int64_t d) { return lds_depth() == 4 ? lds_head<4, float>(d) : lds_head<8, float>(d); }
 
 int launch_sparse_lds_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
                              int updater, int64_t max_nnz, hipStream_t stream, int* kernel_variant) {
     if (kp.n_chains <= 0) return 0;
     if (!sparse_lds_applies(kp.d, max_nnz, kp.n_max)) return -3;
     if (!L.wf32 || L.wstride < (int64_t)kp.d + 128 + 1024) return (int)hipErrorInvalidValue;
-    if (lds_depth() == 8) return lds_launch<8, float>(L, kp, storage, gradient, updater, stream, kernel_variant);
-    return lds_launch<4, float>(L, kp, storage, gradient, updater, stream, kernel_variant);
+    if (lds_depth() == 4) return lds_launch<4, float>(L, kp, storage, gradient, updater, stream, kernel_variant);
+    return lds_launch<8, float>(L, kp, storage, gradient, updater, stream, kernel_variant);
 }
 
 bool sparse_lds64_applies(int64_t d, int64_t max_nnz, int updater, bool check_conv, bool alpha_ok, int64_t n_max) {
     if (max_nnz > LCAP || check_conv || n_max > (int64_t)INT32_MAX) return false;
     if (updater != U_SIMPLE && !(updater == U_SQUARED_L2 && alpha_ok)) return false;
-    return (lds_depth() == 8 ? lds_head<8, double>(d) : lds_head<4, double>(d)) >= 0;
+    return (lds_depth() == 4 ? lds_head<4, double>(d) : lds_head<8, double>(d)) >= 0;
 }
 
 int launch_sparse_lds64_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
@@ -751,8 +840,8 @@ int launch_sparse_lds64_chains(const ChainLaunch& L, const KParams& kp, int stor
     // the chain's f64 vector: [d] + [128] + [1024] doubles inside its slice of L.wf32
     if (!L.wf32 || L.wstride < 2 * ((int64_t)kp.d + 128 + 1024) || (L.wstride & 3) || !L.w_out)
         return (int)hipErrorInvalidValue;
-    if (lds_depth() == 8) return lds_launch<8, double>(L, kp, storage, gradient, updater, stream, kernel_variant);
-    return lds_launch<4, double>(L, kp, storage, gradient, updater, stream, kernel_variant);
+    if (lds_depth() == 4) return lds_launch<4, double>(L, kp, storage, gradient, updater, stream, kernel_variant);
+    return lds_launch<8, double>(L, kp, storage, gradient, updater, stream, kernel_variant);
 }
 
 #endif  // PSGD_NO_DISPATCH
