@@ -390,37 +390,18 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
         }
 
         T2 dsq2 = T2{T(0), T(0)}, nsq2 = T2{T(0), T(0)};
+        if constexpr (UPD == U_ADAM) {
+            // Adam, the reference's variant: v = beta v + (1-beta) g, r = gamma r + (1-gamma) g^2,
+            // fix1 = sqrt(1 - r^iter) + eps, w += -lr * v / fix1. The status first; then, when
+            // 1 - r^iter rounds to exactly 1 for every coordinate of the wave (r^iter below half
+            // an ulp of 1 -- after a few tens of samples for an average of squared gradients
+            // below 1), fix1 is the constant 1 + eps and v / fix1 one multiply by its reciprocal:
+            // the same operations as the general path (whose sqrt of 1 is exactly 1), hoisted.
+            const T beta = T(kp.beta), gamma = T(kp.gamma);
+            T2 vv[E2], rr[E2];
+            bool general = false;
 #pragma unroll
-        for (int e = 0; e < E2; ++e) {
-            const T2 old = w[e];
-            T2 nw;
-            if constexpr (UPD == U_ADAGRAD) {
-                // accum = None ? g*g : accum + g*g; w += -s * (g / sqrt(accum + 1.0))
-                const T2 g = mult * x[e];
-                const T2 acc2 = first ? g * g : ua[e] + g * g;
-                ua[e] = acc2;
-                if constexpr (sizeof(T) == 4) {
-                    nw.x = old.x + a_s * (g.x * __builtin_amdgcn_rsqf(acc2.x + T(1)));
-                    nw.y = old.y + a_s * (g.y * __builtin_amdgcn_rsqf(acc2.y + T(1)));
-                } else {
-                    nw.x = old.x + a_s * (g.x * rsqrt_newton(acc2.x + T(1)));
-                    nw.y = old.y + a_s * (g.y * rsqrt_newton(acc2.y + T(1)));
-                }
-            } else if constexpr (UPD == U_SQUARED_L2) {
-                nw = old * l2c;                     // brzWeights :*= (1 - s*lambda) (UPD.scala:172)
-                nw = nw + a_s * (mult * x[e]);      // axpy(-s, grad, w)
-            } else if constexpr (UPD == U_SIMPLE) {
-                if constexpr (sizeof(T) == 4) nw = __builtin_elementwise_fma(T2{a_s * mult, a_s * mult}, x[e], old);
-                else nw = old + a_s * (mult * x[e]);   // the reference's two roundings (UPD.scala:95)
-            } else if constexpr (UPD == U_L1) {
-                // axpy(-s, grad, w), then soft thresholding by regParam * s (UPD.scala:133-146)
-                nw = old + a_s * (mult * x[e]);
-                nw.x = jsignum(nw.x) * jmax(T(0), m_fabs(nw.x) - shrink);
-                nw.y = jsignum(nw.y) * jmax(T(0), m_fabs(nw.y) - shrink);
-            } else {
-                // Adam, the reference's variant: v = beta v + (1-beta) g, r = gamma r + (1-gamma) g^2,
-                // fix1 = sqrt(1 - r^iter) + eps, w += -lr * v / fix1
-                const T beta = T(kp.beta), gamma = T(kp.gamma);
+            for (int e = 0; e < E2; ++e) {
                 const T2 g = mult * x[e];
                 const T2 sq = g * g;
                 T2 v, r;
@@ -428,21 +409,83 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
                 else { v = ua[e] * beta + g * (T(1) - beta); r = ub[e] * gamma + sq * (T(1) - gamma); }
                 ua[e] = v;
                 ub[e] = r;
+                vv[e] = v;
+                rr[e] = r;
                 if constexpr (sizeof(T) == 4) {
-                    const T fx = __builtin_amdgcn_sqrtf(T(1) - pow_fast(r.x, iter)) + T(kp.eps);
-                    const T fy = __builtin_amdgcn_sqrtf(T(1) - pow_fast(r.y, iter)) + T(kp.eps);
-                    nw.x = old.x + al * (v.x * __builtin_amdgcn_rcpf(fx));
-                    nw.y = old.y + al * (v.y * __builtin_amdgcn_rcpf(fy));
+                    // pow_fast(r, iter) = exp2(iter log2 r) < 2^-26: 1 - r^iter == 1.0f
+                    general |= !(iter * __builtin_amdgcn_logf(r.x) < -26.0f) | !(iter * __builtin_amdgcn_logf(r.y) < -26.0f);
                 } else {
-                    // sqrt and v / fix1 by the hardware estimates + one Newton step (~1e-14)
-                    const T fx = sqrt_newton(one_minus_pow_iter(r.x, iter)) + T(kp.eps);
-                    const T fy = sqrt_newton(one_minus_pow_iter(r.y, iter)) + T(kp.eps);
-                    nw.x = old.x + al * (v.x * recip_newton(fx));
-                    nw.y = old.y + al * (v.y * recip_newton(fy));
+                    // one_minus_pow_iter's own test (it returns exactly 1.0 then)
+                    general |= !((float)iter * __builtin_amdgcn_logf((float)r.x) < -60.0f) |
+                               !((float)iter * __builtin_amdgcn_logf((float)r.y) < -60.0f);
                 }
             }
-            w[e] = nw;
-            if constexpr (CONV) { const T2 df = old - nw; dsq2 += df * df; nsq2 += nw * nw; }
+            if (__builtin_amdgcn_ballot_w64(general) != 0) {
+#pragma unroll
+                for (int e = 0; e < E2; ++e) {
+                    const T2 old = w[e], v = vv[e], r = rr[e];
+                    T2 nw;
+                    if constexpr (sizeof(T) == 4) {
+                        const T fx = __builtin_amdgcn_sqrtf(T(1) - pow_fast(r.x, iter)) + T(kp.eps);
+                        const T fy = __builtin_amdgcn_sqrtf(T(1) - pow_fast(r.y, iter)) + T(kp.eps);
+                        nw.x = old.x + al * (v.x * __builtin_amdgcn_rcpf(fx));
+                        nw.y = old.y + al * (v.y * __builtin_amdgcn_rcpf(fy));
+                    } else {
+                        // sqrt and v / fix1 by the hardware estimates + one Newton step (~1e-14)
+                        const T fx = sqrt_newton(one_minus_pow_iter(r.x, iter)) + T(kp.eps);
+                        const T fy = sqrt_newton(one_minus_pow_iter(r.y, iter)) + T(kp.eps);
+                        nw.x = old.x + al * (v.x * recip_newton(fx));
+                        nw.y = old.y + al * (v.y * recip_newton(fy));
+                    }
+                    w[e] = nw;
+                    if constexpr (CONV) { const T2 df = old - nw; dsq2 += df * df; nsq2 += nw * nw; }
+                }
+            } else {
+                T rfix;
+                if constexpr (sizeof(T) == 4) rfix = __builtin_amdgcn_rcpf(T(1) + T(kp.eps));
+                else rfix = recip_newton(T(1) + T(kp.eps));
+#pragma unroll
+                for (int e = 0; e < E2; ++e) {
+                    const T2 old = w[e], v = vv[e];
+                    T2 nw;
+                    nw.x = old.x + al * (v.x * rfix);
+                    nw.y = old.y + al * (v.y * rfix);
+                    w[e] = nw;
+                    if constexpr (CONV) { const T2 df = old - nw; dsq2 += df * df; nsq2 += nw * nw; }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < E2; ++e) {
+                const T2 old = w[e];
+                T2 nw;
+                if constexpr (UPD == U_ADAGRAD) {
+                    // accum = None ? g*g : accum + g*g; w += -s * (g / sqrt(accum + 1.0))
+                    const T2 g = mult * x[e];
+                    const T2 acc2 = first ? g * g : ua[e] + g * g;
+                    ua[e] = acc2;
+                    if constexpr (sizeof(T) == 4) {
+                        nw.x = old.x + a_s * (g.x * __builtin_amdgcn_rsqf(acc2.x + T(1)));
+                        nw.y = old.y + a_s * (g.y * __builtin_amdgcn_rsqf(acc2.y + T(1)));
+                    } else {
+                        nw.x = old.x + a_s * (g.x * rsqrt_newton(acc2.x + T(1)));
+                        nw.y = old.y + a_s * (g.y * rsqrt_newton(acc2.y + T(1)));
+                    }
+                } else if constexpr (UPD == U_SQUARED_L2) {
+                    nw = old * l2c;                     // brzWeights :*= (1 - s*lambda) (UPD.scala:172)
+                    nw = nw + a_s * (mult * x[e]);      // axpy(-s, grad, w)
+                } else if constexpr (UPD == U_SIMPLE) {
+                    if constexpr (sizeof(T) == 4) nw = __builtin_elementwise_fma(T2{a_s * mult, a_s * mult}, x[e], old);
+                    else nw = old + a_s * (mult * x[e]);   // the reference's two roundings (UPD.scala:95)
+                } else if constexpr (UPD == U_L1) {
+                    // axpy(-s, grad, w), then soft thresholding by regParam * s (UPD.scala:133-146)
+                    nw = old + a_s * (mult * x[e]);
+                    nw.x = jsignum(nw.x) * jmax(T(0), m_fabs(nw.x) - shrink);
+                    nw.y = jsignum(nw.y) * jmax(T(0), m_fabs(nw.y) - shrink);
+                }
+                w[e] = nw;
+                if constexpr (CONV) { const T2 df = old - nw; dsq2 += df * df; nsq2 += nw * nw; }
+            }
         }
         if constexpr (CONV) {
             pdsq = wave_sum_uniform(dsq2.x + dsq2.y);

@@ -1,4 +1,4 @@
-"""Summarise a tools/profile_round.sh output directory into one JSON for profiles/.
+"""Summarise a tools/profile.sh output directory into one JSON for profiles/.
 
 Per kernel (matched by a name prefix): dispatches, average duration from the kernel trace, and
 per-dispatch averages of FETCH_SIZE / WRITE_SIZE / SQ_INSTS_* from the separate --pmc passes.
@@ -22,11 +22,12 @@ import statistics
 
 KERNELS = ("psgd::chain_block64", "psgd::chain_block", "psgd::chain_sparse_spec", "psgd::chain_sparse_lds", "psgd::chain_sparse",
            "psgd::chain_dense", "psgd::chain_split", "psgd::chain_general", "psgd::fold_kernel", "psgd::fold_f32_kernel",
-           "psgd::wf32_init_kernel", "psgd::margin_loss_kernel", "psgd::logistic_loss64_kernel")
+           "psgd::fold_scaled_kernel", "psgd::wf32_init_kernel", "psgd::w64_init_kernel", "psgd::margin_loss_kernel",
+           "psgd::logistic_loss64_kernel")
 
 
 STREAM_KERNELS = ("psgd::chain_block", "psgd::chain_dense", "psgd::chain_split", "psgd::fold_kernel", "psgd::fold_f32_kernel",
-                  "psgd::wf32_init_kernel")
+                  "psgd::fold_scaled_kernel", "psgd::wf32_init_kernel")
 
 
 def read_scale(kernel):
