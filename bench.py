@@ -152,18 +152,21 @@ def parse():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for --gpus > 1: nccl (RCCL over xGMI, one GPU per rank) or "
                          "gloo (a CPU rehearsal of the multi-rank path; ranks may share one GPU)")
+    ap.add_argument("--skew-rows", type=int, default=0,
+                    help="dense shards: start partition p's rows p * K rows later in HBM (layout experiments)")
     ap.add_argument("--prewarm-s", type=float, default=1.0,
                     help="untimed epochs for this long before the warmup steps (GPU clock ramp)")
     return ap.parse_args()
 
 
-def make_shard(torch, dev, n, d, P, grad, dtype, seed):
+def make_shard(torch, dev, n, d, P, grad, dtype, seed, skew=0):
     """Synthetic rows in HBM: X ~ N(0,1); w* ~ N(0, 1/d); LeastSquares y = w*.x + N(0, 0.01);
-    Logistic y = 1{w*.x + Logistic(0,1) > 0}."""
+    Logistic y = 1{w*.x + Logistic(0,1) > 0}. skew > 0: partition p's rows start
+    p * skew rows later in the allocation (unused rows in between)."""
     g = torch.Generator(device=dev)
     g.manual_seed(seed)
     tdt = torch.float32 if dtype == "f32" else torch.float64
-    X = torch.empty((n, d), dtype=tdt, device=dev)
+    X = torch.empty((n + P * skew, d), dtype=tdt, device=dev)
     chunk = 1 << 20
     w_star = torch.randn(d, generator=g, device=dev, dtype=torch.float64) / d ** 0.5
     y = torch.empty(n, dtype=torch.float64, device=dev)
@@ -177,6 +180,11 @@ def make_shard(torch, dev, n, d, P, grad, dtype, seed):
             u = torch.rand(b - a, generator=g, device=dev, dtype=torch.float64).clamp_(1e-12, 1 - 1e-12)
             y[a:b] = ((z + torch.log(u) - torch.log1p(-u)) > 0).to(torch.float64)
     offs = [i * n // P for i in range(P)] + [n]
+    if skew:
+        # move each partition's rows to its skewed place, last partition first
+        for p in range(P - 1, 0, -1):
+            a, b = offs[p], offs[p + 1]
+            X[a + p * skew:b + p * skew] = X[a:b].clone()
     return X, y, offs
 
 
@@ -305,7 +313,8 @@ def cpu_baseline_c1(budget_s, seed=42):
 
 
 def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, rows, fraction,
-                 steps, warmup, prewarm_s, features=0, chains=0, updater="", storage="", backend="nccl"):
+                 steps, warmup, prewarm_s, features=0, chains=0, updater="", storage="", backend="nccl",
+                 skew=0):
     """One workload: synthetic shard in HBM, prewarm, W warmup steps, K timed steps (barrier +
     synchronize on both sides, max over ranks). Returns the measurement as a dict."""
     import numpy as np
@@ -334,9 +343,10 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
         parts = [pkg.DeviceCsrPartition(y[a:b], rp[a:b + 1], col, val, d) for a, b in zip(offs[:-1], offs[1:])]
         empty = lambda: pkg.DeviceCsrPartition(y[:0], rp[:1], col, val, d)
     else:
-        X, y, offs = make_shard(torch, dev, n, d, P, grad, sdt, 1000 + rank)
+        X, y, offs = make_shard(torch, dev, n, d, P, grad, sdt, 1000 + rank, skew)
         torch.cuda.synchronize()
-        parts = [pkg.DevicePartition(y[a:b], X[a:b], d) for a, b in zip(offs[:-1], offs[1:])]
+        parts = [pkg.DevicePartition(y[a:b], X[a + p * skew:b + p * skew], d)
+                 for p, (a, b) in enumerate(zip(offs[:-1], offs[1:]))]
         empty = lambda: pkg.DevicePartition(y[:0], X[:0], d)
     # global partition list: this rank's block is [rank*P, (rank+1)*P)
     all_parts = [None] * (P * world)
@@ -527,7 +537,7 @@ def main():
 
     res = run_workload(torch, dist, pkg, dev, rank, world, local, args.workload, args.compute,
                        args.rows, args.fraction, args.steps, args.warmup, args.prewarm_s, args.features,
-                       args.chains, args.updater, args.storage, args.backend)
+                       args.chains, args.updater, args.storage, args.backend, args.skew_rows)
     grad, d, P, step, csr, upd_name, reg = res.pop("_meta")
     res.pop("loss")
     out = {

@@ -224,8 +224,11 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
     // in wave order. A stopped chain leaves collect with whatever it read (the host raises on the
     // watchdog word).
     constexpr uint64_t kMask = XW == 64 ? ~0ull : ((1ull << XW) - 1);
+    // Every lane writes (no EXEC juggling on the per-sample path): lanes past the wave's PC * KV
+    // words write its last word again, with the same value (the partials are wave-uniform).
     auto publish = [&](const T (&val)[KV], int32_t t) __attribute__((always_inline)) {
-        const int k = lane / PC;
+        const int l = lane < PC * KV ? lane : PC * KV - 1;
+        const int k = l / PC;
         T vk = val[0];
 #pragma unroll
         for (int q = 1; q < KV; ++q) vk = k == q ? val[q] : vk;
@@ -234,10 +237,9 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
             piece = __float_as_uint(vk);
         } else {
             const uint64_t b = (uint64_t)__double_as_longlong(vk);
-            piece = (lane & 1) == 0 ? (uint32_t)b : (uint32_t)(b >> 32);
+            piece = (l & 1) == 0 ? (uint32_t)b : (uint32_t)(b >> 32);
         }
-        if (lane < PC * KV)
-            lds_write_u64(xw + (int)(t & 1) * XW + h * PC * KV + lane, ((uint64_t)(uint32_t)(t + 1) << 32) | piece);
+        lds_write_u64(xw + (int)(t & 1) * XW + h * PC * KV + l, ((uint64_t)(uint32_t)(t + 1) << 32) | piece);
     };
     auto collect = [&](int32_t t, T (&sum)[KV]) __attribute__((always_inline)) {
         const uint32_t tag = (uint32_t)(t + 1);
@@ -569,8 +571,9 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
 }
 
 // ------------------------------------------------------------------------------------------
-// Launcher.
+// Launcher (left out of single-kernel ISA probes, tools/isa_probe.sh).
 // ------------------------------------------------------------------------------------------
+#ifndef PSGD_NO_DISPATCH
 namespace {
 
 template <typename S>
@@ -693,5 +696,7 @@ int launch_split_chains(const ChainLaunch& L, const KParams& kp, int storage, in
     if (compute == 1) return split_dispatch_grad<double, float>(L, kp, gradient, updater, min_ld, max_ld, lds, st, variant);
     return split_dispatch_grad<double, double>(L, kp, gradient, updater, min_ld, max_ld, lds, st, variant);
 }
+
+#endif  // PSGD_NO_DISPATCH
 
 }  // namespace psgd
