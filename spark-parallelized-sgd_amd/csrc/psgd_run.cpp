@@ -69,8 +69,10 @@ void print_array(const char* name, const double* v, size_t n, bool last = false)
 // Checkpoint of the driver loop (--checkpoint FILE; the Python host's DriverCheckpoint): the
 // state between iterations -- next iteration, regVal, whether currentWeights is set, converged,
 // the loss history and the weights -- behind a fingerprint of the parameters and the data shape
-// (numIterations excluded: a finished run can be continued with a larger budget). Written after
-// every iteration to FILE.tmp and renamed over FILE.
+// (numIterations excluded: a finished run can be continued with a larger budget). The fingerprint
+// covers the data's shape (rows, partitions, features), not its values: resuming against another
+// file of the same shape is the caller's mistake to avoid. Written after every iteration to
+// FILE.tmp and renamed over FILE.
 struct LoopState {
     int32_t i = 1;
     double regVal = 0.0;
