@@ -22,11 +22,13 @@ template <int CTRL>
 __device__ __forceinline__ float dpp_mov(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
+// (64-bit adds take no DPP operand: two v_mov_b32_dpp; bound_ctrl writes 0 for a lane without a
+// source, as the old value 0 would, without the two v_mov 0 that an old operand costs)
 template <int CTRL>
 __device__ __forceinline__ double dpp_mov(double v) {
     long long b = __double_as_longlong(v);
-    int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, 0xF, 0xF, false);
-    int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffffll), CTRL, 0xF, 0xF, true);
+    int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, true);
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 

@@ -18,8 +18,10 @@
 // row. Per sample each wave takes its partial dot, reduces it across its lanes and publishes it
 // in LDS as tagged 64-bit words ({32 bits of the partial, sample number + 1}: one word per fp32
 // partial, two per fp64 one), so a reader needs no separate flag: it polls the H words of the
-// sample's parity slot until every tag is the sample's. All waves add the partials in wave order
-// (((p0 + p1) + p2) + p3) -- bit-identical -- run the identical scalar multiplier, and update
+// sample's parity slot until every tag is the sample's. All waves add the partials in one fixed
+// order -- (p0 + p1) + (p2 + p3) by DPP across lane groups when a sample carries one value,
+// ((p0 + p1) + p2) + p3 by readlane with the convergence terms -- bit-identical in every wave,
+// run the identical scalar multiplier, and update
 // only their own features. A parity slot is rewritten two samples later, only after every wave
 // has published the sample in between (which it does after reading this one).
 //
@@ -78,6 +80,12 @@ __device__ __forceinline__ void lds_write_u64(uint64_t* p, uint64_t v) {
 __device__ __forceinline__ uint64_t lds_read_u64(const uint64_t* p) {
     uint64_t v;
     asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"((unsigned)(uintptr_t)p) : "memory");
+    return v;
+}
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4 lds_read_b128(const uint64_t* p) {
+    u32x4 v;
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"((unsigned)(uintptr_t)p) : "memory");
     return v;
 }
 
@@ -241,17 +249,33 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
         }
         lds_write_u64(xw + (int)(t & 1) * XW + h * PC * KV + l, ((uint64_t)(uint32_t)(t + 1) << 32) | piece);
     };
+    // One partial per sample (KV = 1, H = 2 or 4): every lane reads wave (lane % H)'s partial (fp64:
+    // both of its words in one 16-byte read) and the H partials are added across each group of H
+    // lanes by DPP, (p0 + p1) + (p2 + p3) in every lane of every wave (a + b and b + a are the same
+    // bits) -- no readlane and no SGPR round trip on the sample's path.
+    constexpr bool kLaneSum = KV == 1 && (H == 2 || H == 4);
     auto collect = [&](int32_t t, T (&sum)[KV]) __attribute__((always_inline)) {
         const uint32_t tag = (uint32_t)(t + 1);
-        const uint64_t* src = xw + (int)(t & 1) * XW + (lane < XW ? lane : 0);
-        uint64_t v = lds_read_u64(src);
-        if ((__ballot((uint32_t)(v >> 32) == tag) & kMask) != kMask) {
+        const uint64_t* src = xw + (int)(t & 1) * XW + (kLaneSum ? PC * (lane & (H - 1)) : (lane < XW ? lane : 0));
+        constexpr uint64_t kNeed = kLaneSum ? ~0ull : kMask;
+        u32x4 v;   // {piece, tag} (kLaneSum fp64: {low piece, tag, high piece, tag})
+        auto poll = [&]() __attribute__((always_inline)) -> bool {
+            if constexpr (kLaneSum && PC == 2) {
+                v = lds_read_b128(src);
+                return __ballot(v[1] == tag && v[3] == tag) == kNeed;
+            } else {
+                const uint64_t q = lds_read_u64(src);
+                v[0] = (uint32_t)q;
+                v[1] = (uint32_t)(q >> 32);
+                return (__ballot(v[1] == tag) & kNeed) == kNeed;
+            }
+        };
+        if (!poll()) {
             // spin on the LDS words alone (s_memrealtime is a scalar-memory round trip that the
             // next LDS wait would also wait for); the stop flag and the clock every 1024 polls
             uint64_t t0 = 0;
             for (unsigned spin = 1;; ++spin) {
-                v = lds_read_u64(src);
-                if ((__ballot((uint32_t)(v >> 32) == tag) & kMask) == kMask) break;
+                if (poll()) break;
                 if ((spin & 1023) == 0) {
                     if (__hip_atomic_load(&hdr->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == kStopError) { stop = true; break; }
                     const uint64_t now = __builtin_amdgcn_s_memrealtime();
@@ -265,7 +289,16 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
                 }
             }
         }
-        const int lo = (int)(uint32_t)v;
+        if constexpr (kLaneSum) {
+            T pg;
+            if constexpr (PC == 1) pg = __uint_as_float(v[0]);
+            else pg = __longlong_as_double((long long)(((uint64_t)v[2] << 32) | v[0]));
+            T s = pg + dpp_mov<0xB1>(pg);                 // quad_perm [1,0,3,2]
+            if constexpr (H == 4) s = s + dpp_mov<0x4E>(s);   // quad_perm [2,3,0,1]
+            sum[0] = s;
+            return;
+        }
+        const int lo = (int)v[0];
 #pragma unroll
         for (int q = 0; q < KV; ++q) {
             T acc = T(0);
@@ -321,8 +354,10 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
         }
         const T2 a = a0 + a1;
         {
+            // the partial in every lane (permlane swaps, the same bits as wave_sum_uniform's lane
+            // 63): it is stored from VGPRs, so no readlane / v_mov round trip through an SGPR
             T val[KV];
-            val[0] = wave_sum_uniform(a.x + a.y);
+            val[0] = wave_sum(a.x + a.y);
             if constexpr (CONV) { val[1] = pdsq; val[2] = pnsq; }
             publish(val, t);
         }
@@ -401,7 +436,21 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
             // the same operations as the general path (whose sqrt of 1 is exactly 1), hoisted.
             const T beta = T(kp.beta), gamma = T(kp.gamma);
             T2 vv[E2], rr[E2];
-            bool general = false;
+            // The test runs once per lane, on an upper bound of the lane's r values: with gamma in
+            // [0, 1] every r is +0 or more (or NaN), and such floats order as their bit patterns,
+            // so the largest pattern with the sign bit cleared is the largest r, or a NaN when any
+            // r is one (fp64: the high words, completed with all-ones low words: a bound >= every
+            // r). The threshold has half a unit of margin over the per-coordinate test below, so
+            // the bound passing implies every coordinate passing (v_log_f32 need not be strictly
+            // monotone); gamma outside [0, 1] takes the general path.
+            uint32_t rbits = 0;
+            auto rmax = [&](T r) __attribute__((always_inline)) {
+                uint32_t b;
+                if constexpr (sizeof(T) == 4) b = __float_as_uint(r);
+                else b = (uint32_t)((uint64_t)__double_as_longlong(r) >> 32);
+                b &= 0x7FFFFFFFu;
+                rbits = b > rbits ? b : rbits;
+            };
 #pragma unroll
             for (int e = 0; e < E2; ++e) {
                 const T2 g = mult * x[e];
@@ -413,14 +462,17 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
                 ub[e] = r;
                 vv[e] = v;
                 rr[e] = r;
-                if constexpr (sizeof(T) == 4) {
-                    // pow_fast(r, iter) = exp2(iter log2 r) < 2^-26: 1 - r^iter == 1.0f
-                    general |= !(iter * __builtin_amdgcn_logf(r.x) < -26.0f) | !(iter * __builtin_amdgcn_logf(r.y) < -26.0f);
-                } else {
-                    // one_minus_pow_iter's own test (it returns exactly 1.0 then)
-                    general |= !((float)iter * __builtin_amdgcn_logf((float)r.x) < -60.0f) |
-                               !((float)iter * __builtin_amdgcn_logf((float)r.y) < -60.0f);
-                }
+                rmax(r.x);
+                rmax(r.y);
+            }
+            bool general = !(kp.gamma >= 0.0 && kp.gamma <= 1.0);
+            if constexpr (sizeof(T) == 4) {
+                // pow_fast(r, iter) = exp2(iter log2 r) < 2^-26: 1 - r^iter == 1.0f
+                general |= !(iter * __builtin_amdgcn_logf(__uint_as_float(rbits)) < -26.5f);
+            } else {
+                // one_minus_pow_iter's own test (it returns exactly 1.0 then)
+                const double rb = __longlong_as_double((long long)(((uint64_t)rbits << 32) | 0xFFFFFFFFull));
+                general |= !((float)iter * __builtin_amdgcn_logf((float)rb) < -60.5f);
             }
             if (__builtin_amdgcn_ballot_w64(general) != 0) {
 #pragma unroll
@@ -463,8 +515,10 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
                 T2 nw;
                 if constexpr (UPD == U_ADAGRAD) {
                     // accum = None ? g*g : accum + g*g; w += -s * (g / sqrt(accum + 1.0))
+                    // (the status starts at +0, and +0 + g*g is g*g: the first sample's None
+                    // branch without a select)
                     const T2 g = mult * x[e];
-                    const T2 acc2 = first ? g * g : ua[e] + g * g;
+                    const T2 acc2 = ua[e] + g * g;
                     ua[e] = acc2;
                     if constexpr (sizeof(T) == 4) {
                         nw.x = old.x + a_s * (g.x * __builtin_amdgcn_rsqf(acc2.x + T(1)));

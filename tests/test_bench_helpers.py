@@ -39,3 +39,15 @@ def test_workloads_cover_the_baseline_configs():
     grad, n, d, P, step, sdt, _ = bench.WORKLOADS["c2"]
     assert (grad, n, d, P, sdt) == ("least_squares", 10_000_000, 512, 256, "f32")
     assert bench.WORKLOADS["c1"][:4] == ("logistic", 100_000, 100, 4)
+
+
+def test_fp64_csr_lines_find_their_profiles():
+    # c5 in fp64 compute runs chain_sparse64<float, 0, 1> (variant 420): its own PMC summary, not
+    # the fp32 chain_sparse one; c4 with the reference's f64 rows runs chain_sparse_lds<double, double, ...>
+    t, src = bench.pmc_traffic("c5", "logistic", 420, "f32", 20_000_000, compute="f64", updater="squared_l2")
+    assert src and src.endswith("_c5_f64_pmc.json"), src
+    assert 5_000 < t / 20_000_000 < 20_000
+    t4, src4 = bench.pmc_traffic("c4", "hinge", 620, "f64", 20_000_000, compute="f64")
+    assert src4 and src4.endswith("_c4_f64rows_pmc.json"), src4
+    assert bench.kernel_name(420).startswith("chain_sparse64")
+    assert bench.kernel_name(620).startswith("chain_sparse_lds (fp64")
