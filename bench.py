@@ -108,9 +108,10 @@ def kernel_name(variant):
         return (f"chain_split (NV={variant % 10}: per-sample chain, features split over {h} compute waves, "
                 f"partial dots exchanged through LDS)")
     if 700 <= variant < 800:
-        waves = 1 + (variant - 700) // 10
+        waves = 1 + (variant - 700) % 40 // 10
+        brk = ", per-sample isConverged break" if variant >= 740 else ""
         return (f"chain_block64 (NV={variant % 10}: blocked fp64 chain, 8-row Gram blocks, "
-                f"{waves} chain wave{'s' if waves > 1 else ''})")
+                f"{waves} chain wave{'s' if waves > 1 else ''}{brk})")
     if 300 <= variant < 400:
         return f"chain_block (NV={variant - 300}: blocked fp32 chain, 8-row Gram blocks)"
     if 600 <= variant < 700:
@@ -154,6 +155,9 @@ def parse():
                          "gloo (a CPU rehearsal of the multi-rank path; ranks may share one GPU)")
     ap.add_argument("--skew-rows", type=int, default=0,
                     help="dense shards: start partition p's rows p * K rows later in HBM (layout experiments)")
+    ap.add_argument("--tol", type=float, default=0.0,
+                    help="convergenceTol of the headline workload (PSGD.scala:262 per-sample break; the "
+                         "reference's default is 0.001; BASELINE's configs run 0)")
     ap.add_argument("--prewarm-s", type=float, default=1.0,
                     help="untimed epochs for this long before the warmup steps (GPU clock ramp)")
     return ap.parse_args()
@@ -314,7 +318,7 @@ def cpu_baseline_c1(budget_s, seed=42):
 
 def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, rows, fraction,
                  steps, warmup, prewarm_s, features=0, chains=0, updater="", storage="", backend="nccl",
-                 skew=0):
+                 skew=0, tol=0.0):
     """One workload: synthetic shard in HBM, prewarm, W warmup steps, K timed steps (barrier +
     synchronize on both sides, max over ranks). Returns the measurement as a dict."""
     import numpy as np
@@ -363,7 +367,7 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
     if updater:   # the workload with another SGDUpdater plugin (UPD.scala:120-286)
         ucls = {"l1": pkg.L1SGDUpdater, "adagrad": pkg.AdaGradSGDUpdater, "adam": pkg.AdamSGDUpdater,
                 "simple": pkg.SimpleSGDUpdater, "squared_l2": pkg.SquaredL2SGDUpdater}[updater]()
-    params = pkg.make_params(gcls, ucls, step, reg, fraction, 0.0, compute)
+    params = pkg.make_params(gcls, ucls, step, reg, fraction, tol, compute)
     w = engine.weights(np.zeros(d))
     stream = engine.stream  # the engine's kernels and copies all run on this stream
 
@@ -433,9 +437,9 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
         elapsed = float(t.item())
     # `cnt` is the whole job's sample count of the step (the fold sums counts over all ranks)
     samples_per_step = cnt
-    if fraction >= 1.0:
+    if fraction >= 1.0 and tol == 0.0:
         assert samples_per_step == n * world, (samples_per_step, n * world)
-    else:  # sampled batches differ per step: the timed steps' samples
+    else:  # sampled batches, or chains that break early (tol > 0): the timed steps' samples
         samples_per_step = total / steps
     value = samples_per_step * steps / elapsed
     assert np.isfinite(loss), loss
@@ -457,7 +461,7 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
         bytes_per_sample = rowstream if weights_on_chip else offchip
     else:
         bytes_per_sample = (d + 1) * es  # row + label (weights are on chip)
-    local_samples = n if fraction >= 1.0 else samples_per_step / world
+    local_samples = n if fraction >= 1.0 and tol == 0.0 else samples_per_step / world
     # one chain-kernel launch processes every (sampled) row of this GPU's partitions
     achieved = local_samples * bytes_per_sample / avg_kernel_s / 1e9
     upd_name = updater or ("squared_l2" if reg > 0 else "simple")
@@ -472,7 +476,7 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
         "config": {"workload": f"{workload}: {cfg_name}", "rows_per_gpu": n, "d": d,
                    "chains_per_gpu": P, "storage": sdt, "gradient": grad,
                    "updater": updater or ("squared_l2" if reg > 0 else "simple"), "reg_param": reg,
-                   "step_size": step, "convergence_tol": 0.0, "mini_batch_fraction": fraction,
+                   "step_size": step, "convergence_tol": tol, "mini_batch_fraction": fraction,
                    "parallelism": f"dp{world}" + (" (chains sharded, RCCL all-gather + fold per epoch)"
                                                    if backend == "nccl" else
                                                    " (chains sharded, gloo all-gather + fold per epoch: a rehearsal)")},
@@ -537,7 +541,7 @@ def main():
 
     res = run_workload(torch, dist, pkg, dev, rank, world, local, args.workload, args.compute,
                        args.rows, args.fraction, args.steps, args.warmup, args.prewarm_s, args.features,
-                       args.chains, args.updater, args.storage, args.backend, args.skew_rows)
+                       args.chains, args.updater, args.storage, args.backend, args.skew_rows, args.tol)
     grad, d, P, step, csr, upd_name, reg = res.pop("_meta")
     res.pop("loss")
     out = {

@@ -15,9 +15,19 @@
 // f64 for f32 rows), the scalar recurrence with the reference's multipliers (exp and the division
 // of LogisticGradient in f64), the updates. Only sums are reassociated (the wave tree of each dot,
 // the Gram identity above, the fused c*x + w update), which is the fp64 mode's 1e-9 relative bar
-// (DESIGN.md §4); per-chain counts are exact because this kernel runs only without the per-sample
-// convergence test (tol = 0). With tol > 0, and for L1/AdaGrad/Adam, the per-sample kernels of
-// psgd_kernels.hip run.
+// (DESIGN.md §4). L1/AdaGrad/Adam run on the per-sample kernels (psgd_split.hip, psgd_kernels.hip).
+//
+// The per-sample break (tol > 0, CONV; PSGD.scala:262, :324-336): isConverged(w_i, w_{i+1}) after
+// row i's update needs ||w_i - w_{i+1}|| and ||w_{i+1}||, and both follow from scalars the block
+// already has. With w' = a w + c x (a = 1 for Simple), z = x . w (the row's dot) and q = x . x
+// (the Gram diagonal, which the Gram waves add to their slot):
+//     ||w'||^2       = a (a ||w||^2 + 2 c z) + c^2 q
+//     ||w - w'||^2   = b (b ||w||^2 - 2 c z) + c^2 q,   b = 1 - a
+// and the test sqrt(D) < tol max(sqrt(N), 1) is D < tol^2 max(N, 1). ||w||^2 starts exact (the
+// chain waves' partial norms of w_in) and follows the recurrence, in the chain's sample order;
+// only a ratio within ~1e-12 of tol could decide differently from the oracle's sums over the
+// rounded vectors. The first row that passes ends the chain: the rows after it in the block take
+// c = 0, a = 1 (no update, loss or count) and no later block runs.
 //
 // Why blocks in fp64: the per-sample kernel (chain_dense) has the dot's wave reduction, an f64
 // exp and a division and the update on one dependent path per sample (~400 ns at d = 100). Here
@@ -196,8 +206,10 @@ __device__ __forceinline__ int role_of_wave(const unsigned* simd, int w) {
 struct XchgHeader64 {
     unsigned xdone[2];   // blocks whose partial dots chain wave 0 / 1 has published
     unsigned fin[2];     // chain wave 0 / 1 has published its partial ||w||^2
+    unsigned start[2];   // CONV: chain wave 0 / 1 has published its partial ||w_in||^2
+    unsigned pad[2];
 };
-constexpr int kXchgDoubles = 2 * 2 * kB + 2;
+constexpr int kXchgDoubles = 2 * 2 * kB + 2 + 2;
 constexpr size_t kFixed64 = sizeof(RingHeader) + sizeof(GramHeader64) + sizeof(XchgHeader64) +
                             kXchgDoubles * sizeof(double);
 static_assert(kFixed64 % 16 == 0, "the meta and row rings start 16-byte aligned");
@@ -211,7 +223,12 @@ static_assert(kFixed64 % 16 == 0, "the meta and row rings start 16-byte aligned"
 #define PSGD_B64_INTERLEAVE 1
 #endif
 
-template <typename S, int GRAD, int UPD, int NV, bool FULL, int H>
+// doubles per Gram ring slot: the 8x8 triangle, and with the per-sample break the block's 8
+// squared row norms
+template <bool CONV>
+constexpr int gram_slot64() { return kB * kB + (CONV ? kB : 0); }
+
+template <typename S, int GRAD, int UPD, int NV, bool FULL, int H, bool CONV>
 __global__ __launch_bounds__(64 * (3 + H)) __attribute__((amdgpu_waves_per_eu(H, H)))
 void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
     using V = typename Vec16<S>::type;
@@ -226,9 +243,10 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
     constexpr bool CONV1 = F32 && H == 2 && EH <= 8 && PSGD_B64_CONV1;
     // wave roles (role_of_waves): chain waves 0 .. H-1, Gram waves 2 and 3, the loader
     constexpr int kRoleLoader = H == 1 ? 1 : 4;
+    constexpr int GSZ = gram_slot64<CONV>();
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // LDS: [RingHeader 16 B][GramHeader64 16 B][XchgHeader64 16 B][exchange 34 doubles]
-    //      [meta ring MB x 256 B][Gram ring GS x 512 B][row ring R x ROW_BYTES]
+    //      [meta ring MB x 256 B][Gram ring GS x GSZ doubles][row ring R x ROW_BYTES]
     RingHeader* hdr = reinterpret_cast<RingHeader*>(smem);
     GramHeader64* ghdr = reinterpret_cast<GramHeader64*>(smem + sizeof(RingHeader));
     XchgHeader64* xhdr = reinterpret_cast<XchgHeader64*>(smem + sizeof(RingHeader) + sizeof(GramHeader64));
@@ -236,7 +254,7 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
     char* meta_ring = smem + kFixed64;
     double* gring = reinterpret_cast<double*>(meta_ring + geom.meta_blocks * kMetaBlockBytes);
     const int GS = geom.gslots;
-    char* ring = reinterpret_cast<char*>(gring + GS * kB * kB);
+    char* ring = reinterpret_cast<char*>(gring + GS * GSZ);
 
     const int lane = threadIdx.x & 63;
     const int chain = blockIdx.x;
@@ -260,9 +278,11 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
         xhdr->xdone[1] = 0;
         xhdr->fin[0] = 0;
         xhdr->fin[1] = 0;
+        xhdr->start[0] = 0;
+        xhdr->start[1] = 0;
     }
     // entries on and above the diagonal stay zero (the Gram waves write only i < k)
-    for (int i = threadIdx.x; i < GS * kB * kB; i += blockDim.x) gring[i] = 0.0;
+    for (int i = threadIdx.x; i < GS * GSZ; i += blockDim.x) gring[i] = 0.0;
     // every wave's SIMD, for the role assignment (the exchange area is free until the chain starts)
     unsigned* simd_of = reinterpret_cast<unsigned*>(xchg);
     if (lane == 0) simd_of[threadIdx.x >> 6] = wave_simd();
@@ -330,6 +350,9 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
             double acc[kPairs];
 #pragma unroll
             for (int q = 0; q < kPairs; ++q) acc[q] = 0.0;
+            double dg[kB];   // CONV: the rows' squared norms (the Gram diagonal)
+#pragma unroll
+            for (int k = 0; k < kB; ++k) dg[k] = 0.0;
             // one 16-byte vector of every row at a time (f64 rows of a whole block would not
             // fit the registers at NV >= 4)
 #pragma unroll
@@ -345,6 +368,21 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
 #pragma unroll
                         for (int h = 0; h < VEC; ++h) acc[q] = __builtin_fma(xc[k][h], xc[i][h], acc[q]);
             }
+            if constexpr (CONV) {
+                // the diagonal in a pass of its own, one row vector at a time (in the pair pass
+                // its 8 accumulators beside the 28 pushed the wave past its registers; the rows are
+                // read again -- the compiler barrier keeps it from reusing the pair pass's loads)
+                asm volatile("" : : : "memory");
+#pragma unroll
+                for (int k = 0; k < kB; ++k)
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) {
+                        double xk[VEC];
+                        read_vec(base + k * ROW_BYTES, v, xk);
+#pragma unroll
+                        for (int h = 0; h < VEC; ++h) dg[k] = __builtin_fma(xk[h], xk[h], dg[k]);
+                    }
+            }
             // every row of the block has been read: hand its ring slots back
             asm volatile("s_waitcnt lgkmcnt(0)" : : : "memory");
             __hip_atomic_store(&ghdr->gread[gw], done + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -354,10 +392,16 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
 #pragma unroll
             for (int q = kPairs; q < 32; ++q) g[q] = 0.0;
             const double val = reduce32d(g, lane);
-            double* slot = gring + gs * (kB * kB);
+            double* slot = gring + gs * GSZ;
             gs += 2;
             if (gs >= GS) gs -= GS;
             if (goff >= 0) slot[goff] = val;
+            if constexpr (CONV) {
+                // lane l holds row k(l)'s norm (reduce8d's layout); one lane per row writes it
+                const double qn = reduce8d(dg, lane);
+                const int kq = ((lane >> 5) & 1) | (((lane >> 4) & 1) << 1) | (((lane >> 3) & 1) << 2);
+                if ((lane & 7) == 0) slot[kB * kB + kq] = qn;
+            }
             ++done;
             __hip_atomic_store(&ghdr->gdone[gw], done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
@@ -385,6 +429,34 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
             const double wv = as_global(L.w_in)[f < d ? f : 0];
             w[u * VEC + k] = f < d ? wv : 0.0;
         }
+    }
+    // CONV: ||w||^2 of the chain's current weights (the same value in both chain waves), from the
+    // exact partial norms of w_in; tol2 = tol^2
+    double nsq = 0.0;
+    const double tol2 = kp.tol * kp.tol;
+    bool conv_stop = false;   // CONV: a row passed isConverged, the chain has ended
+    if constexpr (CONV) {
+        double a = 0.0;
+#pragma unroll
+        for (int e = 0; e < EH; ++e) a = __builtin_fma(w[e], w[e], a);
+        a = wave_sum(a);
+        if constexpr (H == 2) {
+            if (lane == 0) xchg[2 * 2 * kB + 2 + h] = a;
+            asm volatile("s_waitcnt lgkmcnt(0)" : : : "memory");
+            __hip_atomic_store(&xhdr->start[h], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint64_t tw = __builtin_amdgcn_s_memrealtime();
+            while (!__hip_atomic_load(&xhdr->start[h ^ 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                if (__builtin_amdgcn_s_memrealtime() - tw > kWatchdogTicks) {
+                    __hip_atomic_fetch_or(L.watchdog, 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    break;
+                }
+            }
+            asm volatile("" : : : "memory");   // the partial is read after its flag
+            const double other = xchg[2 * 2 * kB + 2 + (h ^ 1)];
+            a = h == 0 ? a + other : other + a;
+        }
+        nsq = a;
     }
     const int krow = ((lane >> 5) & 1) | (((lane >> 4) & 1) << 1) | (((lane >> 3) & 1) << 2);
     const bool loss_lane = (lane & 7) == 0;   // one copy of every row's loss
@@ -499,7 +571,7 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
             }
         }
         PSGD_STAMP(const uint64_t st_g = __builtin_amdgcn_s_memtime(); st_gr += st_g - st_b;)
-        const double* grow = gring + gs * (kB * kB) + krow * kB;
+        const double* grow = gring + gs * GSZ + krow * kB;
         double G[kB];
 #pragma unroll
         for (int q = 0; q < kB / 2; ++q) {
@@ -507,6 +579,8 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
             G[2 * q] = g2.x;
             G[2 * q + 1] = g2.y;
         }
+        double q = 0.0;   // CONV: the squared norm of this lane's row
+        if constexpr (CONV) q = gring[gs * GSZ + kB * kB + krow];
         if constexpr (H == 2) {
             // the other chain wave's partial of this lane's row: z = p0 + p1 in both waves
             const unsigned need = (unsigned)(b + 1);
@@ -551,14 +625,40 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
                 }
             }
         };
+        bool brk = false;   // CONV: a row of this block passed isConverged
+        int keff = kk;      // the rows taken
 #pragma unroll
         for (int i = 0; i < kB; ++i) {
             c[i] = readlane_d(coef64<GRAD>(z, yv, nsv), row_lane64(i));
             if constexpr (TAIL) c[i] = i < kk ? c[i] : 0.0;
+            if constexpr (CONV) c[i] = brk ? 0.0 : c[i];   // rows after the break are not taken
             if constexpr (UPD == U_SQUARED_L2) {
-                if (krow == i) zf = z;
                 al[i] = readlane_d(alpha, row_lane64(i));
                 if constexpr (TAIL) al[i] = i < kk ? al[i] : 1.0;
+                if constexpr (CONV) al[i] = brk ? 1.0 : al[i];
+            }
+            if constexpr (CONV) {
+                // isConverged(w_i, w_{i+1}) (PSGD.scala:262, :333-335) from the recurrences in the
+                // header: z_i (lane row_lane64(i)'s dot, before this step moves it), q_i, c_i, a_i
+                const double zi = readlane_d(z, row_lane64(i));
+                const double qi = readlane_d(q, row_lane64(i));
+                const double cq = c[i] * c[i] * qi;
+                double nn, dd;
+                if constexpr (UPD == U_SQUARED_L2) {
+                    const double ai = al[i], bi = 1.0 - ai;
+                    nn = ai * __builtin_fma(ai, nsq, 2.0 * c[i] * zi) + cq;
+                    dd = bi * __builtin_fma(bi, nsq, -2.0 * c[i] * zi) + cq;
+                } else {
+                    nn = __builtin_fma(c[i], 2.0 * zi, nsq) + cq;
+                    dd = cq;
+                }
+                nsq = nn > 0.0 ? nn : 0.0;
+                const bool pass = (!TAIL || i < kk) && !brk && dd < tol2 * (nn > 1.0 ? nn : 1.0);
+                keff = pass ? i + 1 : keff;
+                brk = brk || pass;
+            }
+            if constexpr (UPD == U_SQUARED_L2) {
+                if (krow == i) zf = z;
                 if (i + 1 < kB) z = __builtin_fma(c[i], G[i], al[i] * z);
             } else {
                 if (i + 1 < kB) z = __builtin_fma(c[i], G[i], z);
@@ -570,13 +670,14 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
         if constexpr (UPD != U_SQUARED_L2) zf = z;
         if (lead) {
             if constexpr (LOSS_EXT) {
-                if (loss_lane && (!TAIL || krow < kk)) zout[t0 + krow] = zf;
+                if (loss_lane && ((!TAIL && !CONV) || krow < keff)) zout[t0 + krow] = zf;
             } else {
                 const double l = row_loss64<GRAD>(zf, yv);
-                if (loss_lane && (!TAIL || krow < kk)) loss_sum += l;
+                if (loss_lane && ((!TAIL && !CONV) || krow < keff)) loss_sum += l;
             }
         }
-        count += kk;
+        count += keff;
+        if constexpr (CONV) conv_stop = brk;
         if (rpre > ready) ready = rpre;
         PSGD_STAMP(const uint64_t st_c = __builtin_amdgcn_s_memtime(); st_rec += st_c - st_xe;)
 
@@ -596,7 +697,7 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
     using Full = std::integral_constant<bool, false>;
     using Tail = std::integral_constant<bool, true>;
     bool ok = true;
-    for (int64_t b = 0; ok && b < nfull; ++b) {
+    for (int64_t b = 0; ok && !conv_stop && b < nfull; ++b) {
         PSGD_STAMP(const uint64_t st_w = __builtin_amdgcn_s_memtime();)
         ok = wait_rows((b + 1) * kB);
         PSGD_STAMP(st_rd += __builtin_amdgcn_s_memtime() - st_w;)
@@ -604,7 +705,7 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
         load_rows(Full{}, ring + rs * ROW_BYTES, kB);
         ok = block(Full{}, b, kB);
     }
-    if (ok && ntail > 0 && wait_rows(n)) {
+    if (ok && !conv_stop && ntail > 0 && wait_rows(n)) {
         load_rows(Tail{}, ring + rs * ROW_BYTES, ntail);
         block(Tail{}, nfull, ntail);
     }
@@ -666,7 +767,7 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
 // ------------------------------------------------------------------------------------------
 // Launcher.
 // ------------------------------------------------------------------------------------------
-template <typename S, int GRAD, int UPD, int NV, int H>
+template <typename S, int GRAD, int UPD, int NV, int H, bool CONV>
 static int launch_block64(const ChainLaunch& L, const KParams& kp, bool full, size_t lds, hipStream_t st) {
     constexpr int ROW = NV * 1024;
     const size_t budget = lds > 0 ? lds : (size_t)64 * 1024;
@@ -674,7 +775,7 @@ static int launch_block64(const ChainLaunch& L, const KParams& kp, bool full, si
     auto bytes_for = [&](int r) {
         const int mb = (r + kMetaRows - 1) / kMetaRows + 2;
         const int gs = r / kB + 1;
-        return kFixed64 + (size_t)mb * kMetaBlockBytes + (size_t)gs * kB * kB * 8 + (size_t)r * ROW;
+        return kFixed64 + (size_t)mb * kMetaBlockBytes + (size_t)gs * gram_slot64<CONV>() * 8 + (size_t)r * ROW;
     };
     int R = (int)((budget - kFixed64) / ROW) / kB * kB;
     while (R > 0 && bytes_for(R) > budget) R -= kB;
@@ -685,11 +786,11 @@ static int launch_block64(const ChainLaunch& L, const KParams& kp, bool full, si
     const size_t bytes = bytes_for(R);
     const dim3 threads(64 * (3 + H));
     if (full) {
-        auto k = chain_block64<S, GRAD, UPD, NV, true, H>;
+        auto k = chain_block64<S, GRAD, UPD, NV, true, H, CONV>;
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
         hipLaunchKernelGGL(k, dim3(kp.n_chains), threads, bytes, st, L, kp, g);
     } else {
-        auto k = chain_block64<S, GRAD, UPD, NV, false, H>;
+        auto k = chain_block64<S, GRAD, UPD, NV, false, H, CONV>;
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
         hipLaunchKernelGGL(k, dim3(kp.n_chains), threads, bytes, st, L, kp, g);
     }
@@ -702,8 +803,9 @@ static int launch_block64(const ChainLaunch& L, const KParams& kp, bool full, si
 
 #ifndef PSGD_NO_DISPATCH
 // Two chain waves (H = 2) from NV = 2 on; PSGD_B64_WAVES=1 keeps one where its share of a
-// block fits the registers (NV <= 4; A/B measurements). Variant 700 + 10 (H - 1) + NV.
-template <typename S, int GRAD, int UPD>
+// block fits the registers (NV <= 4; A/B measurements). Variant 700 + 40 (per-sample break) +
+// 10 (H - 1) + NV.
+template <typename S, int GRAD, int UPD, bool CONV>
 static int block64_nv(const ChainLaunch& L, const KParams& kp, int64_t min_ld, int64_t max_ld,
                       size_t lds, hipStream_t st, int* variant) {
     constexpr int VEC = 16 / sizeof(S);
@@ -715,19 +817,19 @@ static int block64_nv(const ChainLaunch& L, const KParams& kp, int64_t min_ld, i
     while (nv * 64 * VEC < max_ld) nv *= 2;
     const bool full = min_ld >= (int64_t)nv * 64 * VEC;
     const int H = (nv >= 2 && !(one_wave && nv <= 4)) ? 2 : 1;
-    if (variant) *variant = 700 + 10 * (H - 1) + nv;
+    if (variant) *variant = 700 + (CONV ? 40 : 0) + 10 * (H - 1) + nv;
     if (H == 1) {
         switch (nv) {
-        case 1: return launch_block64<S, GRAD, UPD, 1, 1>(L, kp, full, lds, st);
-        case 2: return launch_block64<S, GRAD, UPD, 2, 1>(L, kp, full, lds, st);
-        case 4: return launch_block64<S, GRAD, UPD, 4, 1>(L, kp, full, lds, st);
+        case 1: return launch_block64<S, GRAD, UPD, 1, 1, CONV>(L, kp, full, lds, st);
+        case 2: return launch_block64<S, GRAD, UPD, 2, 1, CONV>(L, kp, full, lds, st);
+        case 4: return launch_block64<S, GRAD, UPD, 4, 1, CONV>(L, kp, full, lds, st);
         default: return -3;
         }
     }
     switch (nv) {
-    case 2: return launch_block64<S, GRAD, UPD, 2, 2>(L, kp, full, lds, st);
-    case 4: return launch_block64<S, GRAD, UPD, 4, 2>(L, kp, full, lds, st);
-    case 8: return launch_block64<S, GRAD, UPD, 8, 2>(L, kp, full, lds, st);
+    case 2: return launch_block64<S, GRAD, UPD, 2, 2, CONV>(L, kp, full, lds, st);
+    case 4: return launch_block64<S, GRAD, UPD, 4, 2, CONV>(L, kp, full, lds, st);
+    case 8: return launch_block64<S, GRAD, UPD, 8, 2, CONV>(L, kp, full, lds, st);
     default: return -3;
     }
 }
@@ -735,8 +837,14 @@ static int block64_nv(const ChainLaunch& L, const KParams& kp, int64_t min_ld, i
 template <typename S, int GRAD>
 static int block64_upd(const ChainLaunch& L, const KParams& kp, int upd, int64_t min_ld,
                        int64_t max_ld, size_t lds, hipStream_t st, int* variant) {
-    if (upd == U_SIMPLE) return block64_nv<S, GRAD, U_SIMPLE>(L, kp, min_ld, max_ld, lds, st, variant);
-    if (upd == U_SQUARED_L2) return block64_nv<S, GRAD, U_SQUARED_L2>(L, kp, min_ld, max_ld, lds, st, variant);
+    // the per-sample break (tol > 0, PSGD.scala:262) is a template instance of its own
+    const bool conv = kp.tol > 0.0;
+    if (upd == U_SIMPLE)
+        return conv ? block64_nv<S, GRAD, U_SIMPLE, true>(L, kp, min_ld, max_ld, lds, st, variant)
+                    : block64_nv<S, GRAD, U_SIMPLE, false>(L, kp, min_ld, max_ld, lds, st, variant);
+    if (upd == U_SQUARED_L2)
+        return conv ? block64_nv<S, GRAD, U_SQUARED_L2, true>(L, kp, min_ld, max_ld, lds, st, variant)
+                    : block64_nv<S, GRAD, U_SQUARED_L2, false>(L, kp, min_ld, max_ld, lds, st, variant);
     return -3;
 }
 
@@ -753,8 +861,15 @@ static int block64_grad(const ChainLaunch& L, const KParams& kp, int grad, int u
 
 bool block64_path_applies(int layout, int compute, int updater, bool check_conv, int storage,
                           int64_t max_ld) {
+    // any tol: the per-sample break runs in the block recurrence (CONV instances, kp.tol > 0);
+    // PSGD_B64_CONV=0 sends tol > 0 to the per-sample kernels instead (tests of chain_split's
+    // break path, A/B measurements; read at every launch)
+    if (check_conv) {
+        const char* e = getenv("PSGD_B64_CONV");
+        if (e && e[0] == '0') return false;
+    }
     const int vec = storage == 1 ? 4 : 2;
-    return layout == kDense && compute == 0 && !check_conv &&
+    return layout == kDense && compute == 0 &&
            (updater == U_SIMPLE || updater == U_SQUARED_L2) && max_ld <= 8 * 64 * vec;
 }
 

@@ -21,9 +21,9 @@
 // sample's parity slot until every tag is the sample's. All waves add the partials in one fixed
 // order -- (p0 + p1) + (p2 + p3) by DPP across lane groups when a sample carries one value,
 // ((p0 + p1) + p2) + p3 by readlane with the convergence terms -- bit-identical in every wave,
-// run the identical scalar multiplier, and update
-// only their own features. A parity slot is rewritten two samples later, only after every wave
-// has published the sample in between (which it does after reading this one).
+// run the identical scalar multiplier, and update only their own features. A parity slot is
+// rewritten two samples later, only after every wave has published the sample in between (which
+// it does after reading this one).
 //
 // Rows stream through the LDS ring of chain_dense (ring_loader, one loader wave); compute wave 0
 // hands slots back: when it has every partial of sample t, all waves have read row t + 1.
@@ -326,6 +326,7 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
         if constexpr (sizeof(T) == 8) zout = L.zbuf64 + (int64_t)chain * L.zstride;
         else zout = L.zbuf + (int64_t)chain * L.zstride;
     }
+    T zprev = T(0);             // Logistic: the last sample's dot, stored during the next exchange
     const char* slot_ptr = ring;
     const char* const ring_end = ring + geom.rows * ROW_BYTES;
     // CONV: this wave's ||w_old - w_new||^2, ||w_new||^2 of the last update (wave-reduced), the
@@ -383,6 +384,9 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
         read_row(std::integral_constant<int, 1 - p>{}, next_ptr, t + 1);   // past the end: unused
         slot_ptr = next_ptr;
 
+        // the previous sample's dot goes out under this exchange's LDS latency, not between the
+        // exchange and the multiplier (wave 0's extra work delays every wave at the next exchange)
+        if constexpr (ZOUT) { if (h == 0 && lane == 0 && t > 0) zout[t - 1] = zprev; }
         T sums[KV];
         collect(t, sums);
         const T z = sums[0];
@@ -409,7 +413,7 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
             // 1/(1 + exp(margin)) - y, margin = -z; the row's loss from z after the chain
             if constexpr (sizeof(T) == 8) mult = recip_one_plus_exp(-z) - y;
             else mult = __builtin_amdgcn_rcpf(1.0f + __expf(-z)) - y;
-            if (h == 0 && lane == 0) zout[t] = z;
+            zprev = z;
         } else {
             T loss;
             if constexpr (GRAD == G_LEAST_SQUARES) {
@@ -563,6 +567,8 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
     if (t < n && !stop && conv_at == n) sample(std::integral_constant<int, 0>{}, t++);
     // the samples taken: n, or up to the per-sample break (a stopped chain: the host raises)
     const int64_t count = conv_at < n ? conv_at : t;
+    // (after a break at sample t, sample t - 1's dot went out during sample t's exchange)
+    if constexpr (ZOUT) { if (h == 0 && lane == 0 && conv_at == n && count > 0) zout[count - 1] = zprev; }
     if constexpr (sizeof(T) == 4) loss_sum += double(loss_blk);
     // regVal of the chain's last update (PSGD.scala:257): Simple / AdaGrad / Adam 0.0
     // (UPD.scala:97, :221, :266), L1 regParam * ||w||_1 (:147), SquaredL2 0.5 regParam ||w||^2

@@ -51,3 +51,9 @@ def test_fp64_csr_lines_find_their_profiles():
     assert src4 and src4.endswith("_c4_f64rows_pmc.json"), src4
     assert bench.kernel_name(420).startswith("chain_sparse64")
     assert bench.kernel_name(620).startswith("chain_sparse_lds (fp64")
+
+
+def test_block64_break_label():
+    assert bench.kernel_name(712).endswith("2 chain waves)")
+    assert bench.kernel_name(752).endswith("2 chain waves, per-sample isConverged break)")
+    assert bench.kernel_name(741).startswith("chain_block64 (NV=1") and "1 chain wave," in bench.kernel_name(741)

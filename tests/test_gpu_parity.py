@@ -44,11 +44,18 @@ U = {"simple": "SimpleSGDUpdater", "squared_l2": "SquaredL2SGDUpdater", "l1": "L
 
 def stateful_variant(upd, tol, nv):
     """Kernel of a dense per-sample epoch (AdaGrad / Adam / L1 at any tol, every updater at
-    tol > 0): the feature-split chain_split (800 + 10 H + NV, H = min(NV, 4) compute waves) from
-    two row vectors on, else the one-wave chain_dense (100 + NV)."""
+    tol > 0 in fp32 compute or with PSGD_B64_CONV=0): the feature-split chain_split (800 + 10 H +
+    NV, H = min(NV, 4) compute waves) from two row vectors on, else the one-wave chain_dense
+    (100 + NV)."""
     if (upd in ("adagrad", "adam", "l1") or tol > 0.0) and nv >= 2:
         return 800 + 10 * min(nv, 4) + nv
     return 100 + nv
+
+
+def block64_variant(tol, nv):
+    """fp64 Simple / SquaredL2 epochs on dense rows of <= 8 vectors: chain_block64, 700 + 40 (the
+    per-sample break, tol > 0) + 10 (H - 1) + NV, H = 2 chain waves from two row vectors on."""
+    return 700 + (40 if tol > 0.0 else 0) + (10 if nv >= 2 else 0) + nv
 
 
 def data_for(pkg, oracle, case):
@@ -192,7 +199,7 @@ def test_kernel_selection(pkg, oracle):
     for d, dtype, tol, expect in ((100, np.float64, 0.0, 701), (512, np.float32, 0.0, 712),
                                   (1024, np.float32, 0.0, 714), (2048, np.float32, 0.0, 718),
                                   (1024, np.float64, 0.0, 718),
-                                  (100, np.float64, 0.001, 101), (512, np.float32, 0.001, 822),
+                                  (100, np.float64, 0.001, 741), (512, np.float32, 0.001, 752),
                                   (3000, np.float64, 0.0, 200)):
         X, y = synth(rng, 64, d, "logistic", dtype)
         data = pkg.PartitionedData.parallelize(y, X, 2, dtype=dtype)
@@ -518,3 +525,66 @@ def test_dense_fp64_stateful_updaters_in_registers(pkg, oracle, upd, d, storage)
         assert [list(c) for c in counts] == [list(c) for c in cr[: len(counts)]], tag
         assert_close(w, wr, what=tag + " weights")
         assert_close(h, hr, what=tag + " loss")
+
+
+@pytest.mark.parametrize("grad", ["logistic", "least_squares", "hinge"])
+@pytest.mark.parametrize("upd", ["simple", "squared_l2"])
+@pytest.mark.parametrize("d,storage", [(60, np.float64), (200, np.float32), (256, np.float64),
+                                       (700, np.float32), (1024, np.float64), (2048, np.float32)])
+def test_block64_per_sample_break(pkg, oracle, grad, upd, d, storage):
+    """tol > 0 on chain_block64 (fp64 Simple / SquaredL2): the per-sample isConverged break
+    (PSGD.scala:262, :324-336) decided from the block recurrence's norms (psgd_block64.hip header:
+    ||w'||^2 and ||w - w'||^2 from z, c and the Gram diagonal). 64 ragged chains (45-46 rows:
+    full blocks and a tail block) at tols whose breaks fall on every row of a block, and one that
+    breaks few chains: exact per-chain counts and 1e-9 against the oracle."""
+    rng = np.random.default_rng(d + len(grad) * 13 + len(upd))
+    P = 64
+    n = P * 45 + 29
+    X, y = synth(rng, n, d, grad)
+    X = X.astype(storage)
+    data = pkg.PartitionedData.parallelize(y, X, P, dtype=storage)
+    offs = [i * n // P for i in range(P)] + [n]
+    sizes = np.diff(offs)
+    vec = 4 if storage == np.float32 else 2
+    nv = 1
+    while nv * 64 * vec < d:
+        nv *= 2
+    step = {"least_squares": 0.5 / d, "logistic": 4.0 / d, "hinge": 2.0 / d}[grad]
+    rows_hit = set()
+    for tol in (0.01, 0.03, 0.1):
+        w, h, counts = pkg.runParallelizedSGD(data, getattr(pkg, G[grad])(), getattr(pkg, U[upd])(), step, 3,
+                                              0.05, 1.0, np.zeros(d), tol, return_chain_counts=True)
+        assert pkg.optimization.get_context(0).last_kernel() == block64_variant(tol, nv)
+        wr, hr, cr = oracle.run(oracle.Matrix(y, X.astype(np.float64)), offs, grad, upd, step, 3, 0.05,
+                                np.zeros(d), tol=tol, n_threads=8)
+        tag = f"{grad} {upd} d={d} {np.dtype(storage).name} tol={tol}"
+        assert [list(c) for c in counts] == [list(c) for c in cr[: len(counts)]], tag
+        assert_close(w, wr, what=tag + " weights")
+        assert_close(h, hr, what=tag + " loss")
+        rows_hit |= {(c - 1) % 8 for it in cr for c, s in zip(it, sizes) if 0 < c < s}
+    assert len(rows_hit) >= 2, rows_hit   # breaks at more than one row position of a block
+
+
+def test_block64_break_every_block_row(pkg, oracle):
+    """Breaks on each of the 8 rows of a block, in full and tail blocks, with f32 and f64 rows
+    (the H = 1 and H = 2 chain-wave forms), against the oracle's exact counts."""
+    for d, storage, nvh in ((60, np.float64, 1), (700, np.float32, 2)):
+        rng = np.random.default_rng(99 + d)
+        P = 96
+        n = P * 45 + 29
+        X, y = synth(rng, n, d, "logistic")
+        X = X.astype(storage)
+        data = pkg.PartitionedData.parallelize(y, X, P, dtype=storage)
+        offs = [i * n // P for i in range(P)] + [n]
+        sizes = np.diff(offs)
+        hit = set()
+        for tol in (0.01, 0.015, 0.02, 0.03):
+            w, h, counts = pkg.runParallelizedSGD(data, pkg.LogisticGradient(), pkg.SimpleSGDUpdater(),
+                                                  4.0 / d, 2, 0.0, 1.0, np.zeros(d), tol,
+                                                  return_chain_counts=True)
+            wr, hr, cr = oracle.run(oracle.Matrix(y, X.astype(np.float64)), offs, "logistic", "simple",
+                                    4.0 / d, 2, 0.0, np.zeros(d), tol=tol, n_threads=8)
+            assert [list(c) for c in counts] == [list(c) for c in cr[: len(counts)]], (d, tol)
+            assert_close(w, wr, what=f"d={d} tol={tol} weights")
+            hit |= {((c - 1) % 8, c > s // 8 * 8) for it in cr for c, s in zip(it, sizes) if 0 < c < s}
+        assert {r for r, _ in hit} == set(range(8)), (d, sorted(hit))

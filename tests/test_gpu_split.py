@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 from conftest import has_gpu
-from test_gpu_parity import FP32_LOSS_REL, FP32_REL, G, U, assert_close, stateful_variant
+from test_gpu_parity import FP32_LOSS_REL, FP32_REL, G, U, assert_close, block64_variant, stateful_variant
 
 pytestmark = pytest.mark.gpu
 
@@ -112,10 +112,13 @@ def test_split_tiny_and_empty_partitions(pkg, oracle, n, P):
 @pytest.mark.parametrize("grad", ["logistic", "least_squares", "hinge"])
 @pytest.mark.parametrize("d,storage,tol", [(700, np.float32, 0.002), (1024, np.float32, 0.02),
                                            (256, np.float64, 0.005)])
-def test_split_per_sample_convergence(pkg, oracle, grad, upd, d, storage, tol):
+def test_split_per_sample_convergence(pkg, oracle, monkeypatch, grad, upd, d, storage, tol):
     """tol > 0: the per-sample isConverged break (PSGD.scala:262, :324-336) on chain_split, its
     test of sample t - 1 carried by the exchange of sample t; every updater (Simple / SquaredL2
-    take this kernel only with the test). fp64 at 1e-9 with exact per-chain counts."""
+    take this kernel only with the test, and in fp64 only with PSGD_B64_CONV=0: chain_block64
+    runs their break by default, test_gpu_parity.py::test_block64_per_sample_break). fp64 at 1e-9
+    with exact per-chain counts."""
+    monkeypatch.setenv("PSGD_B64_CONV", "0")
     rng = np.random.default_rng(d + 11 * len(grad) + 5 * len(upd))
     X, y = synth(rng, 2400, d, grad)
     n = X.shape[0]
@@ -136,12 +139,14 @@ def test_split_per_sample_convergence(pkg, oracle, grad, upd, d, storage, tol):
 
 @pytest.mark.parametrize("upd", ["l1", "squared_l2"])
 @pytest.mark.parametrize("d,storage", [(1024, np.float32), (256, np.float64)])
-def test_split_break_same_parity_final_exchange(pkg, oracle, upd, d, storage):
+def test_split_break_same_parity_final_exchange(pkg, oracle, monkeypatch, upd, d, storage):
     """The regVal exchange after a per-sample break: a chain that breaks at sample t
     with t = n (mod 2) must not publish its final norms into slot t & 1, which a slower wave may
     still be polling for sample t. Many short chains of ragged lengths (37 / 38 rows) at a tol that
     breaks most of them early: both parities of the break against n occur, every chain's count is
-    exact and the run finishes (no watchdog)."""
+    exact and the run finishes (no watchdog). (fp64 SquaredL2 takes chain_split here only with
+    PSGD_B64_CONV=0.)"""
+    monkeypatch.setenv("PSGD_B64_CONV", "0")
     rng = np.random.default_rng(4242 + d)
     P = 128
     n = P * 37 + 61
