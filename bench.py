@@ -113,7 +113,8 @@ def kernel_name(variant):
         return (f"chain_block64 (NV={variant % 10}: blocked fp64 chain, 8-row Gram blocks, "
                 f"{waves} chain wave{'s' if waves > 1 else ''}{brk})")
     if 300 <= variant < 400:
-        return f"chain_block (NV={variant - 300}: blocked fp32 chain, 8-row Gram blocks)"
+        brk = ", per-sample isConverged break" if variant >= 340 else ""
+        return f"chain_block (NV={variant % 10}: blocked fp32 chain, 8-row Gram blocks{brk})"
     if 600 <= variant < 700:
         prec = "fp64" if (variant % 100) >= 20 else "fp32"
         return (f"chain_sparse_lds ({prec} CSR chain, weights LDS-resident [tail past ~160 KiB: L2-resident, "

@@ -30,7 +30,16 @@
 //                    reduction of 32 values), written as an 8x8 lower-triangular matrix into a
 //                    Gram ring slot in LDS.
 // No MFMA: the Gram triangle is 3.5 dots per row; a 16x16 f32 MFMA tile would spend 16.
+//
+// The per-sample break (tol > 0, CONV; PSGD.scala:262, :324-336) is decided inside the block as in
+// chain_block64 (psgd_block64.hip): with w' = a w + c x, z = x . w and q = x . x (the Gram
+// diagonal, added to the Gram slot), ||w'||^2 = a (a ||w||^2 + 2 c z) + c^2 q and
+// ||w - w'||^2 = b (b ||w||^2 - 2 c z) + c^2 q (b = 1 - a); isConverged is D < tol^2 max(N, 1).
+// ||w||^2 is taken exactly from the registers at every block start (one more wave sum under the
+// dots), so the fp32 recurrence runs over at most 8 rows. The first passing row ends the chain.
 #include "psgd_device.h"
+
+#include <stdlib.h>
 
 namespace psgd {
 
@@ -139,7 +148,11 @@ __device__ __forceinline__ float row_loss(float z, float y, float aux) {
     }
 }
 
-template <typename S, int GRAD, int UPD, int NV, bool FULL>
+// floats per Gram ring slot: the 8x8 triangle, and with the per-sample break the 8 row norms
+template <bool CONV>
+constexpr int gram_slot32() { return kBlk * kBlk + (CONV ? kBlk : 0); }
+
+template <typename S, int GRAD, int UPD, int NV, bool FULL, bool CONV = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void chain_block(ChainLaunch L, KParams kp, RingGeom geom) {
     using V = typename Vec16<S>::type;
     using T2 = float __attribute__((ext_vector_type(2)));
@@ -149,6 +162,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     constexpr int H = VEC / 2;             // pairs per 16-byte vector
     constexpr int ROW_BYTES = NV * 1024;
     constexpr bool KEEP = E2 * kBlk <= 64; // the chain wave keeps a block's rows in registers
+    constexpr int GSZ = gram_slot32<CONV>();
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // LDS: [RingHeader 16 B][GramHeader 16 B][meta ring MB x 256 B][Gram ring GS x 256 B]
     //      [row ring R x ROW_BYTES]
@@ -157,7 +171,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     char* meta_ring = smem + sizeof(RingHeader) + sizeof(GramHeader);
     float* gring = reinterpret_cast<float*>(meta_ring + geom.meta_blocks * kMetaBlockBytes);
     const int GS = geom.gslots;
-    char* ring = reinterpret_cast<char*>(gring + GS * kBlk * kBlk);
+    char* ring = reinterpret_cast<char*>(gring + GS * GSZ);
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -179,7 +193,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         ghdr->gread[1] = 0;
     }
     // entries on and above the diagonal stay zero (the Gram waves write only i < k)
-    for (int i = threadIdx.x; i < GS * kBlk * kBlk; i += blockDim.x) gring[i] = 0.0f;
+    for (int i = threadIdx.x; i < GS * GSZ; i += blockDim.x) gring[i] = 0.0f;
     __syncthreads();
 
     if (wave == 1) {
@@ -263,6 +277,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             T2 acc[kPairs];
 #pragma unroll
             for (int q = 0; q < kPairs; ++q) acc[q] = T2{0.0f, 0.0f};
+            T2 dg[CONV ? kBlk : 1];   // CONV: the rows' squared norms (the Gram diagonal)
+#pragma unroll
+            for (int k = 0; k < (CONV ? kBlk : 1); ++k) dg[k] = T2{0.0f, 0.0f};
 #pragma unroll
             for (int v = 0; v < NV; ++v) {
                 auto& xc = xall[v];
@@ -274,6 +291,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
                         for (int h = 0; h < H; ++h)
                             acc[q] = __builtin_elementwise_fma(xc[k][h], xc[i][h], acc[q]);
+                if constexpr (CONV) {
+#pragma unroll
+                    for (int k = 0; k < kBlk; ++k)
+#pragma unroll
+                        for (int h = 0; h < H; ++h) dg[k] = __builtin_elementwise_fma(xc[k][h], xc[k][h], dg[k]);
+                }
             }
             float g[32];
 #pragma unroll
@@ -282,10 +305,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             for (int q = kPairs; q < 32; ++q) g[q] = 0.0f;
             float val = reduce32(g, lane);
             if constexpr (GRAD == G_LOGISTIC) val *= kNegLog2e;   // the chain works on u
-            float* slot = gring + gs * (kBlk * kBlk);
+            float* slot = gring + gs * GSZ;
             gs += 2;
             if (gs >= GS) gs -= GS;
             if (goff >= 0) slot[goff] = val;
+            if constexpr (CONV) {
+                // unscaled (the break test uses the real norms); reduce8's layout, one lane per row
+                float dv[kBlk];
+#pragma unroll
+                for (int k = 0; k < kBlk; ++k) dv[k] = dg[k].x + dg[k].y;
+                const float qn = reduce8(dv, lane);
+                const int kq = ((lane >> 5) & 1) | (((lane >> 4) & 1) << 1) | (((lane >> 3) & 1) << 2);
+                if ((lane & 7) == 0) slot[kBlk * kBlk + kq] = qn;
+            }
             ++done;
             __hip_atomic_store(&ghdr->gdone[gw], done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             if constexpr (!EARLY)
@@ -324,6 +356,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     int rs = 0, gs = 0, ms = 0;      // ring slot, Gram slot and meta block of the current block
     const int64_t nfull = n / kBlk;
     const int ntail = (int)(n - nfull * kBlk);
+    const float tol2 = float(kp.tol * kp.tol);
+    bool conv_stop = false;   // CONV: a row passed isConverged, the chain has ended
     PSGD_STAMP(const uint64_t st_begin = __builtin_amdgcn_s_memtime(); uint64_t st_rd = 0, st_gr = 0, st_p = 0, st_rec = 0, st_upd = 0;)
 
     auto wait_rows = [&](int64_t rows) __attribute__((always_inline)) -> bool {
@@ -390,6 +424,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             }
             pk[k] = a.x + a.y;
         }
+        // CONV: ||W||^2 at the block start, exact from the registers (the recurrence below then
+        // spans at most this block's 8 rows)
+        float nsq = 0.0f;
+        if constexpr (CONV) {
+            T2 a = w[0] * w[0];
+#pragma unroll
+            for (int e = 1; e < E2; ++e) a = __builtin_elementwise_fma(w[e], w[e], a);
+            nsq = wave_sum(a.x + a.y);
+        }
         const float yv = float(meta.x), sv = float(meta.y);
         const float nsv = -sv;
         float aux;
@@ -419,23 +462,51 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             }
         }
         PSGD_STAMP(st_gr += __builtin_amdgcn_s_memtime() - st_g;)
-        const float* grow = gring + gs * (kBlk * kBlk) + krow * kBlk;
+        const float* grow = gring + gs * GSZ + krow * kBlk;
         const f32x4 g0 = *reinterpret_cast<const f32x4*>(grow);
         const f32x4 g1 = *reinterpret_cast<const f32x4*>(grow + 4);
         const float G[kBlk] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+        float q = 0.0f;   // CONV: the squared norm of this lane's row
+        if constexpr (CONV) q = gring[gs * GSZ + kBlk * kBlk + krow];
 
         // the scalar recurrence: c_i from z_i, then every later row's dot moves by c_i G[k][i]
         // (SquaredL2 also shrinks the finished rows' z: zf keeps z_k for the loss)
         float c[kBlk], al[kBlk];
         float zf = z;
+        bool brk = false;   // CONV: a row of this block passed isConverged
+        int keff = kk;      // the rows taken
 #pragma unroll
         for (int i = 0; i < kBlk; ++i) {
             c[i] = readlane_f(coef<GRAD>(z, yv, sv, nsv, aux), row_lane(i));
             if constexpr (TAIL) c[i] = i < kk ? c[i] : 0.0f;
+            if constexpr (CONV) c[i] = brk ? 0.0f : c[i];   // rows after the break are not taken
             if constexpr (UPD == U_SQUARED_L2) {
-                if (krow == i) zf = z;
                 al[i] = readlane_f(alpha, row_lane(i));
                 if constexpr (TAIL) al[i] = i < kk ? al[i] : 1.0f;
+                if constexpr (CONV) al[i] = brk ? 1.0f : al[i];
+            }
+            if constexpr (CONV) {
+                // isConverged(w_i, w_{i+1}) from z_i (Logistic: the recurrence carries u), q_i, c_i
+                float zi = readlane_f(z, row_lane(i));
+                if constexpr (GRAD == G_LOGISTIC) zi *= kLn2Neg;
+                const float qi = readlane_f(q, row_lane(i));
+                const float cq = c[i] * c[i] * qi;
+                float nn, dd;
+                if constexpr (UPD == U_SQUARED_L2) {
+                    const float ai = al[i], bi = 1.0f - ai;
+                    nn = ai * __builtin_fmaf(ai, nsq, 2.0f * c[i] * zi) + cq;
+                    dd = bi * __builtin_fmaf(bi, nsq, -2.0f * c[i] * zi) + cq;
+                } else {
+                    nn = __builtin_fmaf(c[i], 2.0f * zi, nsq) + cq;
+                    dd = cq;
+                }
+                nsq = nn > 0.0f ? nn : 0.0f;
+                const bool pass = (!TAIL || i < kk) && !brk && dd < tol2 * (nn > 1.0f ? nn : 1.0f);
+                keff = pass ? i + 1 : keff;
+                brk = brk || pass;
+            }
+            if constexpr (UPD == U_SQUARED_L2) {
+                if (krow == i) zf = z;
                 if (i + 1 < kBlk) z = __builtin_fmaf(c[i], G[i], al[i] * z);
             } else {
                 if (i + 1 < kBlk) z = __builtin_fmaf(c[i], G[i], z);
@@ -444,13 +515,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if constexpr (UPD != U_SQUARED_L2) zf = z;
         PSGD_STAMP(const uint64_t st_c = __builtin_amdgcn_s_memtime(); st_rec += st_c - st_b;)
         if constexpr (LOSS_EXT) {
-            if (loss_lane && (!TAIL || krow < kk)) zout[t0 + krow] = zf * kLn2Neg;   // u -> dot
+            if (loss_lane && ((!TAIL && !CONV) || krow < keff)) zout[t0 + krow] = zf * kLn2Neg;   // u -> dot
         } else {
             const float l = row_loss<GRAD>(zf, yv, aux);
-            if (loss_lane && (!TAIL || krow < kk)) loss_blk += l;
+            if (loss_lane && ((!TAIL && !CONV) || krow < keff)) loss_blk += l;
             if ((b & 3) == 3) { loss_sum += double(loss_blk); loss_blk = 0.0f; }
         }
-        count += kk;
+        count += keff;
+        if constexpr (CONV) conv_stop = brk;
         if (rpre > ready) ready = rpre;   // the next block's wait_rows rarely reads the flag again
 
         // W <- a_i W + c_i x_i, i = 0..kk-1, in sample order
@@ -497,14 +569,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     using Tail = std::integral_constant<bool, true>;
     T2 xr[kBlk][E2];
     bool ok = true;
-    for (int64_t b = 0; ok && b < nfull; ++b) {
+    for (int64_t b = 0; ok && !conv_stop && b < nfull; ++b) {
         ok = wait_rows((b + 1) * kBlk);
         if (!ok) break;
         const char* base = ring + rs * ROW_BYTES;
         if constexpr (KEEP) load_rows(Full{}, xr, base, kBlk);
         ok = block(Full{}, xr, b, kBlk, base);
     }
-    if (ok && ntail > 0 && wait_rows(n)) {
+    if (ok && !conv_stop && ntail > 0 && wait_rows(n)) {
         const char* base = ring + rs * ROW_BYTES;
         if constexpr (KEEP) load_rows(Tail{}, xr, base, ntail);
         block(Tail{}, xr, nfull, ntail, base);
@@ -589,7 +661,7 @@ int launch_margin_loss(const ChainLaunch& L, int n_chains, hipStream_t st) {
 // ------------------------------------------------------------------------------------------
 // Launcher.
 // ------------------------------------------------------------------------------------------
-template <typename S, int GRAD, int UPD, int NV>
+template <typename S, int GRAD, int UPD, int NV, bool CONV>
 static int launch_block(const ChainLaunch& L, const KParams& kp, bool full, size_t lds, hipStream_t st) {
     constexpr int ROW = NV * 1024;
     const size_t budget = lds > 0 ? lds : (size_t)64 * 1024;
@@ -599,7 +671,7 @@ static int launch_block(const ChainLaunch& L, const KParams& kp, bool full, size
     auto bytes_for = [&](int r) {
         const int mb = (r + kMetaRows - 1) / kMetaRows + 2;
         const int gs = r / kBlk + 1;
-        return fixed + (size_t)mb * kMetaBlockBytes + (size_t)gs * kBlk * kBlk * 4 + (size_t)r * ROW;
+        return fixed + (size_t)mb * kMetaBlockBytes + (size_t)gs * gram_slot32<CONV>() * 4 + (size_t)r * ROW;
     };
     // a block never wraps (R multiple of kBlk); one block beyond the loader's depth keeps the
     // stream going while the chain wave holds a block
@@ -611,11 +683,11 @@ static int launch_block(const ChainLaunch& L, const KParams& kp, bool full, size
     RingGeom g{R, MB, D, GS};
     const size_t bytes = bytes_for(R);
     if (full) {
-        auto k = chain_block<S, GRAD, UPD, NV, true>;
+        auto k = chain_block<S, GRAD, UPD, NV, true, CONV>;
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
         hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(256), bytes, st, L, kp, g);
     } else {
-        auto k = chain_block<S, GRAD, UPD, NV, false>;
+        auto k = chain_block<S, GRAD, UPD, NV, false, CONV>;
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
         hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(256), bytes, st, L, kp, g);
     }
@@ -628,19 +700,20 @@ static int launch_block(const ChainLaunch& L, const KParams& kp, bool full, size
 
 // The dispatch over every instantiation (left out of the diagnostic build, tools/chain_bench.hip).
 #ifndef PSGD_NO_DISPATCH
-template <typename S, int GRAD, int UPD>
+// Variant 300 + 40 (the per-sample break, tol > 0) + NV.
+template <typename S, int GRAD, int UPD, bool CONV>
 static int block_nv(const ChainLaunch& L, const KParams& kp, int64_t min_ld, int64_t max_ld,
                     size_t lds, hipStream_t st, int* variant) {
     constexpr int VEC = 16 / sizeof(S);
     int nv = 1;
     while (nv * 64 * VEC < max_ld) nv *= 2;
     const bool full = min_ld >= (int64_t)nv * 64 * VEC;
-    if (variant) *variant = 300 + nv;
+    if (variant) *variant = 300 + (CONV ? 40 : 0) + nv;
     switch (nv) {
-    case 1: return launch_block<S, GRAD, UPD, 1>(L, kp, full, lds, st);
-    case 2: return launch_block<S, GRAD, UPD, 2>(L, kp, full, lds, st);
-    case 4: return launch_block<S, GRAD, UPD, 4>(L, kp, full, lds, st);
-    case 8: return launch_block<S, GRAD, UPD, 8>(L, kp, full, lds, st);
+    case 1: return launch_block<S, GRAD, UPD, 1, CONV>(L, kp, full, lds, st);
+    case 2: return launch_block<S, GRAD, UPD, 2, CONV>(L, kp, full, lds, st);
+    case 4: return launch_block<S, GRAD, UPD, 4, CONV>(L, kp, full, lds, st);
+    case 8: return launch_block<S, GRAD, UPD, 8, CONV>(L, kp, full, lds, st);
     default: return -3;
     }
 }
@@ -648,8 +721,13 @@ static int block_nv(const ChainLaunch& L, const KParams& kp, int64_t min_ld, int
 template <typename S, int GRAD>
 static int block_upd(const ChainLaunch& L, const KParams& kp, int upd, int64_t min_ld,
                      int64_t max_ld, size_t lds, hipStream_t st, int* variant) {
-    if (upd == U_SIMPLE) return block_nv<S, GRAD, U_SIMPLE>(L, kp, min_ld, max_ld, lds, st, variant);
-    if (upd == U_SQUARED_L2) return block_nv<S, GRAD, U_SQUARED_L2>(L, kp, min_ld, max_ld, lds, st, variant);
+    const bool conv = kp.tol > 0.0;   // the per-sample break: a template instance of its own
+    if (upd == U_SIMPLE)
+        return conv ? block_nv<S, GRAD, U_SIMPLE, true>(L, kp, min_ld, max_ld, lds, st, variant)
+                    : block_nv<S, GRAD, U_SIMPLE, false>(L, kp, min_ld, max_ld, lds, st, variant);
+    if (upd == U_SQUARED_L2)
+        return conv ? block_nv<S, GRAD, U_SQUARED_L2, true>(L, kp, min_ld, max_ld, lds, st, variant)
+                    : block_nv<S, GRAD, U_SQUARED_L2, false>(L, kp, min_ld, max_ld, lds, st, variant);
     return -3;
 }
 
@@ -666,8 +744,14 @@ static int block_grad(const ChainLaunch& L, const KParams& kp, int grad, int upd
 
 bool block_path_applies(int layout, int compute, int updater, bool check_conv, int storage,
                         int64_t max_ld) {
+    // any tol (CONV instances when kp.tol > 0); PSGD_B64_CONV=0 keeps tol > 0 on the per-sample
+    // kernels, as for chain_block64 (read at every launch)
+    if (check_conv) {
+        const char* e = getenv("PSGD_B64_CONV");
+        if (e && e[0] == '0') return false;
+    }
     const int vec = storage == 1 ? 4 : 2;
-    return layout == kDense && compute == 1 && !check_conv &&
+    return layout == kDense && compute == 1 &&
            (updater == U_SIMPLE || updater == U_SQUARED_L2) && max_ld <= 8 * 64 * vec;
 }
 

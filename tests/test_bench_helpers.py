@@ -57,3 +57,4 @@ def test_block64_break_label():
     assert bench.kernel_name(712).endswith("2 chain waves)")
     assert bench.kernel_name(752).endswith("2 chain waves, per-sample isConverged break)")
     assert bench.kernel_name(741).startswith("chain_block64 (NV=1") and "1 chain wave," in bench.kernel_name(741)
+    assert bench.kernel_name(342) == "chain_block (NV=2: blocked fp32 chain, 8-row Gram blocks, per-sample isConverged break)"
