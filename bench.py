@@ -116,9 +116,10 @@ def kernel_name(variant):
         brk = ", per-sample isConverged break" if variant >= 340 else ""
         return f"chain_block (NV={variant % 10}: blocked fp32 chain, 8-row Gram blocks{brk})"
     if 600 <= variant < 700:
-        prec = "fp64" if (variant % 100) >= 20 else "fp32"
+        prec = "fp64" if (variant - 600) % 40 >= 20 else "fp32"
+        brk = ", per-sample isConverged break" if variant >= 640 else ""
         return (f"chain_sparse_lds ({prec} CSR chain, weights LDS-resident [tail past ~160 KiB: L2-resident, "
-                f"gathered {8 if (variant % 20) >= 10 else 4} samples ahead with an LDS feature-tag correction])")
+                f"gathered {8 if (variant % 20) >= 10 else 4} samples ahead with an LDS feature-tag correction]{brk})")
     if 420 <= variant < 430:
         return ("chain_sparse64 (fp64 CSR chain, weights as double vectors in HBM, alpha-scaled SquaredL2, "
                 "one gather round trip per sample)")

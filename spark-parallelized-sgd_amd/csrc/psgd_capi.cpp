@@ -997,13 +997,15 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
     if (layout == psgd::kCsr && params->compute_dtype == PSGD_F64 && !mn &&
         (psgd::sparse_lds64_applies(d, max_nnz, params->updater, conv, true, n_max) ||
          psgd::sparse64_path_applies(layout, 0, params->updater, conv, true))) {
-        // the fp64 CSR kernels' per-chain f64 vectors (d + 1152 doubles, in L.wf32's memory) and
-        // chain_sparse64's alphas
+        // the fp64 CSR kernels' per-chain f64 vectors (d + 1152 doubles, in L.wf32's memory),
+        // chain_sparse64's alphas, and ||w_in||^2 for the per-sample break
         L.wstride = 2 * (((int64_t)d + 128 + 1024 + 63) / 64 * 64);
         HIP_TRY(ctx->wf32.ensure((size_t)P * (size_t)L.wstride * sizeof(float)));
         HIP_TRY(ctx->walpha.ensure((size_t)P * sizeof(double)));
+        HIP_TRY(ctx->wnsq0.ensure(sizeof(double)));
         L.wf32 = ctx->wf32.as<float>();
         L.walpha = ctx->walpha.as<double>();
+        L.wnsq0 = ctx->wnsq0.as<double>();
     }
     if (params->gradient == PSGD_GRADIENT_LOGISTIC && params->compute_dtype == PSGD_F32 &&
         layout == psgd::kDense) {

@@ -119,6 +119,8 @@ int launch_steps(double step, int64_t n, double* steps, hipStream_t stream);
 bool sparse_path_applies(int layout, int compute, int updater, bool check_conv);
 int launch_sparse_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
                          int updater, int64_t max_nnz, hipStream_t stream, int* kernel_variant);
+// *L.wnsq0 = ||w_in||^2 in f64 (round_f32: of float(w_in), the fp32 kernels' weights).
+int launch_wnsq0(const ChainLaunch& L, int d, bool round_f32, hipStream_t st);
 // The fp64 CSR chain with HBM-resident weights (psgd_sparse.hip, chain_sparse64): Simple, and
 // SquaredL2 when kp.alpha_ok; the chain's double vector lives in its slice of L.wf32 (>= 2 (d +
 // 1152) floats), its alpha in L.walpha; weights end there (w = walpha v, launch_fold_f64).

@@ -381,18 +381,29 @@ __global__ __launch_bounds__(64) void chain_general(ChainLaunch L, KParams kp) {
     const gmut<double> SB = L.state ? SA + d : nullptr;
     const gmut<double> SC = (L.state && LAYOUT == kCsr) ? SA + 2 * d : nullptr;
 
-    for (int i = lane; i < d; i += 64) W[i] = as_global(L.w_in)[i];
+    // CSR rows with Simple / SquaredL2 and the per-sample break: ||w||^2 is carried from sample to
+    // sample (O(nnz) per sample instead of a pass over all d): Simple adds each changed
+    // coordinate's nw^2 - old^2; SquaredL2 (lazy form below) the recurrence of chain_block64,
+    // ||w'||^2 = a (a ||w||^2 + 2 c z) + c^2 q, ||w - w'||^2 = b (b ||w||^2 - 2 c z) + c^2 q
+    // (a = 1 - s lambda, b = 1 - a, c = -s mult, z = x . w, q = x . x). Starts from ||w_in||^2.
+    constexpr bool NORMS = CONV && LAYOUT == kCsr && (UPD == U_SIMPLE || UPD == U_SQUARED_L2);
+    double wn = 0.0;
+    for (int i = lane; i < d; i += 64) {
+        const double v = as_global(L.w_in)[i];
+        W[i] = v;
+        if constexpr (NORMS) wn += v * v;
+    }
     if constexpr (LAYOUT == kCsr && UPD == U_ADAM)
         for (int i = lane; i < d; i += 64) SC[i] = 0.0;
     wave_mem_fence();
+    if constexpr (NORMS) wn = wave_sum(wn);
 
-    // CSR rows with SquaredL2 and no per-sample convergence test: the alpha-scaled lazy form
-    // (SURVEY §8a a7). The chain keeps w = alpha * v, so the reference's O(d) scale
-    // w *= 1 - s*lambda (UPD.scala:169) is one multiply of alpha and the gradient step adds
-    // (-s g_j) / alpha to v_j at the row's indices; alpha is folded back into v (O(d)) when it
-    // leaves [2^-400, 2^400] or becomes 0, and at the chain's end. Equal to the reference's
-    // arithmetic up to rounding (the 1e-9 fp64 bar).
-    constexpr bool LAZY = LAYOUT == kCsr && UPD == U_SQUARED_L2 && !CONV;
+    // CSR rows with SquaredL2: the alpha-scaled lazy form. The chain keeps
+    // w = alpha * v, so the reference's O(d) scale w *= 1 - s*lambda (UPD.scala:169) is one
+    // multiply of alpha and the gradient step adds (-s g_j) / alpha to v_j at the row's indices;
+    // alpha is folded back into v (O(d)) when it leaves [2^-400, 2^400] or becomes 0, and at the
+    // chain's end. Equal to the reference's arithmetic up to rounding (the 1e-9 fp64 bar).
+    constexpr bool LAZY = LAYOUT == kCsr && UPD == U_SQUARED_L2;
     double alpha = 1.0;
     double loss_sum = 0.0;
     int64_t count = 0;
@@ -404,6 +415,7 @@ __global__ __launch_bounds__(64) void chain_general(ChainLaunch L, KParams kp) {
         int64_t kb = 0, ke = 0;
         // dot(data, weights)
         double acc = 0.0;
+        [[maybe_unused]] double qacc = 0.0;   // NORMS + SquaredL2: x . x
         const int64_t ri = dsc.rows ? (int64_t)as_global(dsc.rows)[t] : t;   // sampled epoch
         if constexpr (LAYOUT == kDense) {
             xr = X + ri * dsc.ld;
@@ -411,10 +423,18 @@ __global__ __launch_bounds__(64) void chain_general(ChainLaunch L, KParams kp) {
         } else {
             kb = ROWP[ri];
             ke = ROWP[ri + 1];
-            for (int64_t k = kb + lane; k < ke; k += 64)
+            for (int64_t k = kb + lane; k < ke; k += 64) {
                 acc = m_fma(double(X[k]), W[COL[k]], acc);
+                if constexpr (NORMS && UPD == U_SQUARED_L2) qacc = m_fma(double(X[k]), double(X[k]), qacc);
+            }
         }
-        double z = wave_sum(acc);
+        double z;
+        if constexpr (NORMS && UPD == U_SQUARED_L2) {
+            wave_sum2(acc, qacc);
+            z = acc;
+        } else {
+            z = wave_sum(acc);
+        }
         if constexpr (LAZY) z = alpha * z;   // dot(x, w) with w = alpha * v
         double mult;
         const double loss = gradient_scalar<GRAD, double>(z, y, mult);
@@ -430,11 +450,11 @@ __global__ __launch_bounds__(64) void chain_general(ChainLaunch L, KParams kp) {
                 const double old = W[i];
                 const double nw = old + a * (mult * double(X[k]));
                 W[i] = nw;
-                if constexpr (CONV) { const double df = old - nw; dsq += df * df; }
-            }
-            if constexpr (CONV) {
-                wave_mem_fence();
-                for (int i = lane; i < d; i += 64) nsq += W[i] * W[i];
+                if constexpr (CONV) {
+                    const double df = old - nw;
+                    dsq += df * df;
+                    nsq += nw * nw - old * old;   // the change of ||w||^2 (NORMS)
+                }
             }
         } else {
             if constexpr (LAYOUT == kCsr) {
@@ -443,6 +463,13 @@ __global__ __launch_bounds__(64) void chain_general(ChainLaunch L, KParams kp) {
                 // the reference: L2 scales before the axpy, L1 thresholds after it).
                 if constexpr (LAZY) {
                     const double c = 1.0 - s * kp.reg;
+                    if constexpr (NORMS) {
+                        // ||w'||^2 and ||w - w'||^2 from the recurrence (header of this branch)
+                        const double cc = a * mult, b = 1.0 - c, cq = cc * cc * qacc;
+                        const double nn = c * __builtin_fma(c, wn, 2.0 * cc * z) + cq;
+                        dsq = b * __builtin_fma(b, wn, -2.0 * cc * z) + cq;
+                        nsq = nn > 0.0 ? nn : 0.0;
+                    }
                     const double na = alpha * c;
                     if (!(__builtin_fabs(na) >= 0x1p-400 && __builtin_fabs(na) <= 0x1p400)) {
                         for (int i = lane; i < d; i += 64) W[i] = (alpha * W[i]) * c;
@@ -529,7 +556,7 @@ __global__ __launch_bounds__(64) void chain_general(ChainLaunch L, KParams kp) {
                     wave_mem_fence();
                     for (int64_t k = kb + lane; k < ke; k += 64) SC[COL[k]] = 0.0;
                 }
-                if constexpr (CONV && (UPD == U_SQUARED_L2 || UPD == U_L1)) {
+                if constexpr (CONV && UPD == U_L1) {   // (SquaredL2: the lazy form's recurrence)
                     wave_mem_fence();
                     for (int i = lane; i < d; i += 64) {
                         const double nw = W[i];
@@ -601,7 +628,15 @@ __global__ __launch_bounds__(64) void chain_general(ChainLaunch L, KParams kp) {
             }
         }
         wave_mem_fence();
-        if constexpr (CONV) {
+        if constexpr (NORMS && UPD == U_SQUARED_L2) {
+            // dsq and nsq are the recurrence's (wave-uniform)
+            wn = nsq;
+            if (sqrt(dsq > 0.0 ? dsq : 0.0) < kp.tol * jmax(sqrt(nsq), 1.0)) break;
+        } else if constexpr (NORMS) {
+            wave_sum2(dsq, nsq);
+            wn = wn + nsq;
+            if (sqrt(dsq) < kp.tol * jmax(sqrt(wn), 1.0)) break;
+        } else if constexpr (CONV) {
             wave_sum2(dsq, nsq);
             if (sqrt(dsq) < kp.tol * jmax(sqrt(nsq), 1.0)) break;
         }
@@ -933,7 +968,9 @@ int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int stora
                                    stream, kernel_variant);
     if (!per_sample && sparse_path_applies(layout, compute, updater, check_conv)) {
         if (weights_in) *weights_in = kWeightsF32;
-        return launch_sparse_chains(L, kp, storage, gradient, updater, max_nnz, stream, kernel_variant);
+        const int e = launch_sparse_chains(L, kp, storage, gradient, updater, max_nnz, stream, kernel_variant);
+        if (e != -3) return e;
+        if (weights_in) *weights_in = kWeightsOut;   // tol > 0 past the LDS kernel's range
     }
     // PSGD_SPARSE_KERNEL=hbm64 keeps fp64 CSR epochs off the LDS kernel (tests, A/B measurements;
     // read at every launch)

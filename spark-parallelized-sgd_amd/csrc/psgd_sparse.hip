@@ -623,9 +623,11 @@ size_t spec_lds_bytes(int d) {
     return sizeof(SpecHeader) + SR * sizeof(SpecSlot) + (((size_t)d * 2 + 15) / 16) * 16;
 }
 
+// any tol: with the per-sample break (tol > 0) only chain_sparse_lds applies (launch_sparse_chains
+// returns -3 otherwise and the caller falls through to chain_general)
 bool sparse_path_applies(int layout, int compute, int updater, bool check_conv) {
-    return layout == kCsr && compute == 1 && !check_conv &&
-           (updater == U_SIMPLE || updater == U_SQUARED_L2);
+    (void)check_conv;
+    return layout == kCsr && compute == 1 && (updater == U_SIMPLE || updater == U_SQUARED_L2);
 }
 
 template <typename S, int GRAD>
@@ -677,7 +679,8 @@ static int spec_launch(const ChainLaunch& L, const KParams& kp, int storage, int
 // Epoch set-up of the fp32 CSR chains: every chain's fp32 weights = float(w_in), written by the
 // whole GPU (a slice of w_in is read once per block and stored to a range of chains), instead of
 // by each chain's one wave before its first sample (2^22 features x 1024 chains = 17 GB);
-// wnsq0 = ||float(w_in)||^2 in f64 (SquaredL2; one block, fixed tree: deterministic).
+// wnsq0 = ||float(w_in)||^2 in f64 (SquaredL2 and the per-sample break; one block, fixed tree:
+// deterministic; the fp64 kernels' break takes ||w_in||^2 itself, round_f32 = false).
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void wf32_init_kernel(float* __restrict__ wf, int64_t wstride,
                                                         const double* __restrict__ w_in, int d,
@@ -701,11 +704,11 @@ __global__ __launch_bounds__(256) void wf32_init_kernel(float* __restrict__ wf, 
 }
 
 __global__ __launch_bounds__(1024) void wnsq0_kernel(const double* __restrict__ w_in, int d,
-                                                     double* __restrict__ out) {
+                                                     double* __restrict__ out, bool round_f32) {
     __shared__ double s[1024];
     double t = 0.0;
     for (int i = threadIdx.x; i < d; i += 1024) {
-        const double v = double(float(w_in[i]));
+        const double v = round_f32 ? double(float(w_in[i])) : w_in[i];
         t += v * v;
     }
     s[threadIdx.x] = t;
@@ -717,6 +720,11 @@ __global__ __launch_bounds__(1024) void wnsq0_kernel(const double* __restrict__ 
     if (threadIdx.x == 0) *out = s[0];
 }
 
+int launch_wnsq0(const ChainLaunch& L, int d, bool round_f32, hipStream_t st) {
+    hipLaunchKernelGGL(wnsq0_kernel, dim3(1), dim3(1024), 0, st, L.w_in, d, L.wnsq0, round_f32);
+    return (int)hipGetLastError();
+}
+
 static int sparse_epoch_init(const ChainLaunch& L, const KParams& kp, int updater, hipStream_t st) {
     const int bx = (kp.d + 1023) / 1024;
     int by = (2048 + bx - 1) / bx;          // >= 2048 blocks in all
@@ -725,8 +733,7 @@ static int sparse_epoch_init(const ChainLaunch& L, const KParams& kp, int update
     by = (kp.n_chains + per - 1) / per;
     hipLaunchKernelGGL(wf32_init_kernel, dim3(bx, by), dim3(256), 0, st, L.wf32, L.wstride, L.w_in,
                        kp.d, kp.n_chains, per);
-    if (updater == U_SQUARED_L2)
-        hipLaunchKernelGGL(wnsq0_kernel, dim3(1), dim3(1024), 0, st, L.w_in, kp.d, L.wnsq0);
+    if (updater == U_SQUARED_L2 || kp.tol > 0.0) return launch_wnsq0(L, kp.d, true, st);
     return (int)hipGetLastError();
 }
 
@@ -810,6 +817,8 @@ int launch_sparse_chains(const ChainLaunch& L, const KParams& kp, int storage, i
         rc = launch_sparse_lds_chains(L, kp, storage, gradient, updater, max_nnz, stream, kernel_variant);
         if (rc != -3) return rc;
     }
+    // the HBM-weight fp32 kernels have no per-sample break
+    if (kp.tol > 0.0) return -3;
     if (!no_spec && max_nnz <= SCAP && spec_lds_bytes<8, 32>(kp.d) <= 160 * 1024) {
         if (kernel_variant) *kernel_variant = 410 + storage;
         return spec_launch<8, 32>(L, kp, storage, gradient, updater, stream);

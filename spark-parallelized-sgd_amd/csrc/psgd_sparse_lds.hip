@@ -40,6 +40,14 @@
 //                   read/write addresses (rw) into the slot.
 // Rows are published through LDS counters: loaded (loader), tagged (tagger), done (chain).
 // No MFMA: the work per sample is a ~100-long gather-dot and scatter.
+//
+// The per-sample break (tol > 0, CONV; PSGD.scala:262, :324-336): the chain wave tests
+// isConverged after every sample from scalars it has -- with w' = a w + c x (a = 1 - s lambda for
+// SquaredL2, else 1), z = x . w and q = x . x (one more wave sum beside the dot's),
+// ||w'||^2 = a (a ||w||^2 + 2 c z) + c^2 q and ||w - w'||^2 = b (b ||w||^2 - 2 c z) + c^2 q
+// (b = 1 - a), in f64 from ||w_in||^2 (L.wnsq0), as chain_block64 does; the test is
+// D < tol^2 max(N, 1). After the first passing sample the rest of its unrolled group runs with
+// c = 0 (no update, loss or count) and the chain ends.
 #include "psgd_device.h"
 
 #include <stdlib.h>
@@ -150,7 +158,7 @@ int64_t lds_head(int64_t d) {
 
 // TAIL = false: every feature is in LDS (K = d), the chain issues no VMEM at all.
 // T: the weights' and the arithmetic's type (float: the fp32 throughput mode; double: fp64).
-template <typename S, typename T, int GRAD, int UPD, int SK, bool TAIL>
+template <typename S, typename T, int GRAD, int UPD, int SK, bool TAIL, bool CONV = false>
 __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams kp, int K) {
     constexpr bool L2 = UPD == U_SQUARED_L2;
     constexpr bool F64 = sizeof(T) == 8;
@@ -469,6 +477,11 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
     // one's registers could be reused while the load is still in flight.
     double alpha = 1.0;       // SquaredL2: w = alpha * v
     double dnsq = 0.0;        // SquaredL2, fp32: ||v||^2 - ||v_0||^2 (this lane)
+    // CONV: ||w||^2 (the recurrence in the header), the break state and the samples taken
+    double nsq = CONV ? *L.wnsq0 : 0.0;
+    const double tol2 = kp.tol * kp.tol;
+    bool brk = false;
+    int32_t taken = 0;
     double loss_sum = 0.0;
     float loss_blk = 0.0f;
     int64_t count = 0;
@@ -569,11 +582,15 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
         T acc = cur.x0 * w0;
         acc = m_fma(cur.x1, w1, acc);
         T z = wave_sum_uniform(acc);
+        T qx = T(0);   // CONV: x . x
+        if constexpr (CONV) qx = wave_sum_uniform(m_fma(cur.x1, cur.x1, cur.x0 * cur.x0));
+        // CONV: a sample after the break is not taken (c = 0, no shrink, no loss)
+        [[maybe_unused]] const bool live = !CONV || !brk;
         if constexpr (L2) {
             // w = alpha v: the dot is alpha (x . v); then the L2 shrink alpha *= 1 - s lambda
             // (SGDUpdater.scala:176) and the step adds c x_j / alpha to v
             z = T(alpha * double(z));
-            alpha *= 1.0 - cur.s64 * kp.reg;
+            alpha *= live ? 1.0 - cur.s64 * kp.reg : 1.0;
         }
         T c;
         if constexpr (F64) {
@@ -581,12 +598,30 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
             double mult;
             const double loss = gradient_scalar<GRAD, double>(z, cur.y, mult);
             c = -cur.s * mult;
-            loss_sum += t < n ? loss : 0.0;
+            loss_sum += t < n && live ? loss : 0.0;
         } else {
             float loss;
             c = sparse_coef<GRAD>(z, cur.y, cur.s, loss);
-            loss_blk += t < n ? loss : 0.0f;
+            loss_blk += t < n && live ? loss : 0.0f;
             if ((t & 31) == 31) { loss_sum += double(loss_blk); loss_blk = 0.0f; }
+        }
+        if constexpr (CONV) {
+            c = live ? c : T(0);
+            // isConverged(w_t, w_{t+1}) (PSGD.scala:262, :333-335) from z, q, c (f64)
+            const double cd = double(c), zd = double(z), cq = cd * cd * double(qx);
+            double nn, dd;
+            if constexpr (L2) {
+                const double a = live ? 1.0 - cur.s64 * kp.reg : 1.0, b = 1.0 - a;
+                nn = a * __builtin_fma(a, nsq, 2.0 * cd * zd) + cq;
+                dd = b * __builtin_fma(b, nsq, -2.0 * cd * zd) + cq;
+            } else {
+                nn = __builtin_fma(cd, 2.0 * zd, nsq) + cq;
+                dd = cq;
+            }
+            nsq = nn > 0.0 ? nn : 0.0;
+            const bool pass = t < n && live && dd < tol2 * (nn > 1.0 ? nn : 1.0);
+            taken = pass ? t + 1 : taken;
+            brk = brk || pass;
         }
         const T cv = L2 ? T(double(c) / alpha) : c;
         const T nv0 = m_fma(cv, cur.x0, w0);
@@ -608,9 +643,9 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
         publish(&hdr->done, t + 1);
         cur = nxt;
     };
-    for (int32_t t = 0; ok && t < n_pad; t += GS)
+    for (int32_t t = 0; ok && !brk && t < n_pad; t += GS)
         static_for<GS>([&](auto qc) { sample(qc, t + decltype(qc)::value); });
-    count = ok ? n : 0;
+    count = ok ? (brk ? taken : n) : 0;
     __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // the last gathers' registers stay allocated until they have landed
@@ -676,15 +711,24 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
 
 // The dispatch over every instantiation (left out of single-kernel ISA probes, tools/isa_probe.sh).
 #ifndef PSGD_NO_DISPATCH
-template <typename S, typename T, int GRAD, int SK>
-static int lds_upd(const ChainLaunch& L, const KParams& kp, int upd, int K, size_t lds, hipStream_t st) {
-    auto k = K < kp.d ? (upd == U_SIMPLE ? chain_sparse_lds<S, T, GRAD, U_SIMPLE, SK, true>
-                                         : chain_sparse_lds<S, T, GRAD, U_SQUARED_L2, SK, true>)
-                      : (upd == U_SIMPLE ? chain_sparse_lds<S, T, GRAD, U_SIMPLE, SK, false>
-                                         : chain_sparse_lds<S, T, GRAD, U_SQUARED_L2, SK, false>);
+template <typename S, typename T, int GRAD, int SK, bool CONV>
+static int lds_upd_c(const ChainLaunch& L, const KParams& kp, int upd, int K, size_t lds, hipStream_t st) {
+    auto k = K < kp.d ? (upd == U_SIMPLE ? chain_sparse_lds<S, T, GRAD, U_SIMPLE, SK, true, CONV>
+                                         : chain_sparse_lds<S, T, GRAD, U_SQUARED_L2, SK, true, CONV>)
+                      : (upd == U_SIMPLE ? chain_sparse_lds<S, T, GRAD, U_SIMPLE, SK, false, CONV>
+                                         : chain_sparse_lds<S, T, GRAD, U_SQUARED_L2, SK, false, CONV>);
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(192), lds, st, L, kp, K);
     return (int)hipGetLastError();
+}
+
+// the per-sample break (tol > 0) has instances at the default depth SK = 4 only
+template <typename S, typename T, int GRAD, int SK>
+static int lds_upd(const ChainLaunch& L, const KParams& kp, int upd, int K, size_t lds, hipStream_t st) {
+    if constexpr (SK == 4) {
+        if (kp.tol > 0.0) return lds_upd_c<S, T, GRAD, SK, true>(L, kp, upd, K, lds, st);
+    }
+    return lds_upd_c<S, T, GRAD, SK, false>(L, kp, upd, K, lds, st);
 }
 
 template <typename S, typename T, int SK>
@@ -697,7 +741,8 @@ static int lds_grad(const ChainLaunch& L, const KParams& kp, int grad, int upd, 
     }
 }
 
-// Variant 600 + 10 (SK == 8) + 20 (fp64 compute) + storage (1: f32 rows).
+// Variant 600 + 40 (the per-sample break, tol > 0) + 10 (SK == 8) + 20 (fp64 compute) + storage
+// (1: f32 rows).
 template <int SK, typename T>
 static int lds_launch(const ChainLaunch& L, const KParams& kp, int storage, int gradient, int updater,
                       hipStream_t stream, int* kernel_variant) {
@@ -707,7 +752,7 @@ static int lds_launch(const ChainLaunch& L, const KParams& kp, int storage, int 
     if (const char* e = getenv("PSGD_SPARSE_LDS_HEAD"))
         if (*e) { const int64_t cap = atoll(e) & ~int64_t(3); if (cap >= 0 && cap < K) K = cap; }
     const size_t lds = (size_t)lds_bytes<SK, T>(kp.d, K);
-    if (kernel_variant) *kernel_variant = 600 + (SK == 8 ? 10 : 0) + (sizeof(T) == 8 ? 20 : 0) + storage;
+    if (kernel_variant) *kernel_variant = 600 + (kp.tol > 0.0 ? 40 : 0) + (SK == 8 ? 10 : 0) + (sizeof(T) == 8 ? 20 : 0) + storage;
     if (storage == 1) return lds_grad<float, T, SK>(L, kp, gradient, updater, (int)K, lds, stream);
     return lds_grad<double, T, SK>(L, kp, gradient, updater, (int)K, lds, stream);
 }
@@ -734,12 +779,14 @@ int launch_sparse_lds_chains(const ChainLaunch& L, const KParams& kp, int storag
     if (kp.n_chains <= 0) return 0;
     if (!sparse_lds_applies(kp.d, max_nnz, kp.n_max)) return -3;
     if (!L.wf32 || L.wstride < (int64_t)kp.d + 128 + 1024) return (int)hipErrorInvalidValue;
-    if (lds_depth() == 8) return lds_launch<8, float>(L, kp, storage, gradient, updater, stream, kernel_variant);
+    if (kp.tol > 0.0 && !L.wnsq0) return (int)hipErrorInvalidValue;
+    if (lds_depth() == 8 && kp.tol <= 0.0) return lds_launch<8, float>(L, kp, storage, gradient, updater, stream, kernel_variant);
     return lds_launch<4, float>(L, kp, storage, gradient, updater, stream, kernel_variant);
 }
 
 bool sparse_lds64_applies(int64_t d, int64_t max_nnz, int updater, bool check_conv, bool alpha_ok, int64_t n_max) {
-    if (max_nnz > LCAP || check_conv || n_max > (int64_t)INT32_MAX) return false;
+    (void)check_conv;   // any tol: the per-sample break is a CONV instance (kp.tol > 0)
+    if (max_nnz > LCAP || n_max > (int64_t)INT32_MAX) return false;
     if (updater != U_SIMPLE && !(updater == U_SQUARED_L2 && alpha_ok)) return false;
     return (lds_depth() == 8 ? lds_head<8, double>(d) : lds_head<4, double>(d)) >= 0;
 }
@@ -751,7 +798,13 @@ int launch_sparse_lds64_chains(const ChainLaunch& L, const KParams& kp, int stor
     // the chain's f64 vector: [d] + [128] + [1024] doubles inside its slice of L.wf32
     if (!L.wf32 || L.wstride < 2 * ((int64_t)kp.d + 128 + 1024) || (L.wstride & 3) || !L.w_out)
         return (int)hipErrorInvalidValue;
-    if (lds_depth() == 8) return lds_launch<8, double>(L, kp, storage, gradient, updater, stream, kernel_variant);
+    if (kp.tol > 0.0) {
+        // ||w_in||^2 for the per-sample break's norm recurrence
+        if (!L.wnsq0) return (int)hipErrorInvalidValue;
+        const int e = launch_wnsq0(L, kp.d, false, stream);
+        if (e) return e;
+    }
+    if (lds_depth() == 8 && kp.tol <= 0.0) return lds_launch<8, double>(L, kp, storage, gradient, updater, stream, kernel_variant);
     return lds_launch<4, double>(L, kp, storage, gradient, updater, stream, kernel_variant);
 }
 

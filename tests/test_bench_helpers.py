@@ -58,3 +58,5 @@ def test_block64_break_label():
     assert bench.kernel_name(752).endswith("2 chain waves, per-sample isConverged break)")
     assert bench.kernel_name(741).startswith("chain_block64 (NV=1") and "1 chain wave," in bench.kernel_name(741)
     assert bench.kernel_name(342) == "chain_block (NV=2: blocked fp32 chain, 8-row Gram blocks, per-sample isConverged break)"
+    assert bench.kernel_name(661).startswith("chain_sparse_lds (fp64") and bench.kernel_name(661).endswith("break)")
+    assert bench.kernel_name(641).startswith("chain_sparse_lds (fp32") and "gathered 4" in bench.kernel_name(641)

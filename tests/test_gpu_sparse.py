@@ -281,3 +281,112 @@ def test_sparse_fp64_beyond_lds(pkg, oracle, grad):
     offs = [0, 1000, 1000, 1001, 2200, 3000]
     check64(pkg, oracle, rp, col, val, y, d, offs, grad, "squared_l2", 0.4, 0.01, 3, want=420)
     check64(pkg, oracle, rp, col, val, y, d, offs, grad, "simple", 0.4, 0.0, 2, dtype=np.float32, want=421)
+
+
+# ------------------------------------------------------------------------------------------
+# The per-sample break (tol > 0, PSGD.scala:262, :324-336) on chain_sparse_lds (variant 640 +
+# ...): the chain wave tests isConverged from z, x.x, c and the ||w||^2 recurrence. fp64: exact
+# per-chain counts and 1e-9; fp32: chain by chain against the fp64 oracle (a break may land a
+# row off across the rounding). Step 1.0 with tols 0.01 / 0.03 / 0.1 gives chains that never
+# break, break early and break late for every gradient (checked on the oracle).
+# ------------------------------------------------------------------------------------------
+def break_case(rng, grad, P=64):
+    n = P * 45 + 29
+    d = 3000
+    rp, col, val, y = synth_csr(rng, n, d, 5, 40, grad)
+    offs = [i * n // P for i in range(P)] + [n]
+    return rp, col, val, y, d, offs
+
+
+@pytest.mark.parametrize("grad", ["least_squares", "logistic", "hinge"])
+@pytest.mark.parametrize("upd", ["simple", "squared_l2"])
+@pytest.mark.parametrize("head", ["all", "third"])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_sparse_lds64_per_sample_break(pkg, oracle, monkeypatch, grad, upd, head, dtype):
+    from test_gpu_parity import assert_close
+    monkeypatch.delenv("PSGD_SPARSE_KERNEL", raising=False)
+    monkeypatch.delenv("PSGD_SPARSE_SK", raising=False)
+    rng = np.random.default_rng(len(grad) * 5 + len(upd))
+    rp, col, val, y, d, offs = break_case(rng, grad)
+    if head == "third":
+        monkeypatch.setenv("PSGD_SPARSE_LDS_HEAD", str(d // 3))
+    else:
+        monkeypatch.delenv("PSGD_SPARSE_LDS_HEAD", raising=False)
+    vstore = val.astype(dtype)
+    parts = [pkg.CsrPartition(y[a:b], rp[a:b + 1] - rp[a], col[rp[a]:rp[b]], vstore[rp[a]:rp[b]], d)
+             for a, b in zip(offs[:-1], offs[1:])]
+    data = pkg.PartitionedData(parts)
+    mat = oracle.Matrix(y, row_ptr=rp, col=col, val=vstore.astype(np.float64), d=d)
+    breaks = 0
+    for tol in (0.01, 0.03, 0.1):
+        w, h, counts = pkg.runParallelizedSGD(data, getattr(pkg, G[grad])(), getattr(pkg, U[upd])(), 1.0, 3,
+                                              0.05, 1.0, np.zeros(d), tol, return_chain_counts=True)
+        assert pkg.optimization.get_context(0).last_kernel() == 660 + (1 if dtype == np.float32 else 0)
+        wr, hr, cr = oracle.run(mat, offs, grad, upd, 1.0, 3, 0.05, np.zeros(d), tol=tol, n_threads=8)
+        tag = f"fp64 {grad} {upd} head={head} tol={tol}"
+        assert [list(c) for c in counts] == [list(c) for c in cr[: len(counts)]], tag
+        assert_close(w, wr, what=tag + " weights")
+        assert_close(h, hr, what=tag + " loss")
+        breaks += sum(int(c < s) for it in cr for c, s in zip(it, np.diff(offs)))
+    assert breaks > 0
+
+
+@pytest.mark.parametrize("grad", ["least_squares", "logistic", "hinge"])
+@pytest.mark.parametrize("upd", ["simple", "squared_l2"])
+@pytest.mark.parametrize("head", ["all", "third"])
+def test_sparse_lds_per_sample_break_fp32(pkg, oracle, monkeypatch, grad, upd, head):
+    for k in ("PSGD_SPARSE_KERNEL", "PSGD_SPARSE_SK", "PSGD_SPARSE_LDS_HEAD"):
+        monkeypatch.delenv(k, raising=False)
+    rng = np.random.default_rng(len(grad) * 5 + len(upd))
+    rp, col, val, y, d, offs = break_case(rng, grad)
+    if head == "third":
+        monkeypatch.setenv("PSGD_SPARSE_LDS_HEAD", str(d // 3))
+    vstore = val.astype(np.float32)
+    parts = [pkg.CsrPartition(y[a:b], rp[a:b + 1] - rp[a], col[rp[a]:rp[b]], vstore[rp[a]:rp[b]], d)
+             for a, b in zip(offs[:-1], offs[1:])]
+    data = pkg.PartitionedData(parts)
+    mat = oracle.Matrix(y, row_ptr=rp, col=col, val=vstore.astype(np.float64), d=d)
+    for tol in (0.01, 0.03, 0.1):
+        w, h, counts = pkg.runParallelizedSGD(data, getattr(pkg, G[grad])(), getattr(pkg, U[upd])(), 1.0, 3,
+                                              0.05, 1.0, np.zeros(d), tol, compute_dtype="f32",
+                                              return_chain_counts=True)
+        assert pkg.optimization.get_context(0).last_kernel() == 641
+        wr, hr, cr = oracle.run(mat, offs, grad, upd, 1.0, 3, 0.05, np.zeros(d), tol=tol, n_threads=8)
+        tag = f"fp32 {grad} {upd} head={head} tol={tol}"
+        got = [c for it in counts for c in it]
+        ref = [c for it in cr[: len(counts)] for c in it]
+        same = sum(int(a == b) for a, b in zip(got, ref))
+        assert len(got) == len(ref) and same >= 0.9 * len(ref), (tag, same, len(ref))
+        if same == len(ref) and len(h) == len(hr):
+            scale = max(np.max(np.abs(wr)), 1e-30)
+            assert np.max(np.abs(w - wr)) / scale <= FP32_REL, tag
+            assert np.max(np.abs(h - hr) / np.maximum(np.abs(hr), 1e-30)) <= FP32_LOSS_REL, tag
+
+
+@pytest.mark.parametrize("compute", ["f32", "f64"])
+@pytest.mark.parametrize("upd", ["simple", "squared_l2"])
+def test_sparse_break_beyond_lds_takes_chain_general(pkg, oracle, monkeypatch, compute, upd):
+    """tol > 0 with d past the LDS kernel's range: the HBM-weight kernels have no per-sample
+    break, so chain_general runs it, carrying ||w||^2 from sample to sample (O(nnz) per sample,
+    SquaredL2 in its lazy alpha-scaled form with the norm recurrence); exact in fp64."""
+    from test_gpu_parity import assert_close
+    for k in ("PSGD_SPARSE_KERNEL", "PSGD_SPARSE_SK", "PSGD_SPARSE_LDS_HEAD"):
+        monkeypatch.delenv(k, raising=False)
+    rng = np.random.default_rng(77)
+    n, d = 300, 200_000
+    rp, col, val, y = synth_csr(rng, n, d, 5, 40, "logistic")
+    offs = [0, 150, 300]
+    parts = [pkg.CsrPartition(y[a:b], rp[a:b + 1] - rp[a], col[rp[a]:rp[b]], val[rp[a]:rp[b]], d)
+             for a, b in zip(offs[:-1], offs[1:])]
+    reg = 0.05 if upd == "squared_l2" else 0.0
+    w, h, counts = pkg.runParallelizedSGD(pkg.PartitionedData(parts), pkg.LogisticGradient(),
+                                          getattr(pkg, U[upd])(), 1.0, 2, reg, 1.0, np.zeros(d), 0.1,
+                                          compute_dtype=compute, return_chain_counts=True)
+    assert pkg.optimization.get_context(0).last_kernel() == 201
+    wr, hr, cr = oracle.run(oracle.Matrix(y, row_ptr=rp, col=col, val=val, d=d), offs, "logistic", upd,
+                            1.0, 2, reg, np.zeros(d), tol=0.1, n_threads=8)
+    assert sum(int(c < s) for it in cr for c, s in zip(it, np.diff(offs))) > 0   # breaks happen
+    if compute == "f64":
+        assert [list(c) for c in counts] == [list(c) for c in cr[: len(counts)]]
+        assert_close(w, wr, what="beyond-LDS break weights")
+        assert_close(h, hr, what="beyond-LDS break loss")
