@@ -120,14 +120,16 @@ def kernel_name(variant):
         brk = ", per-sample isConverged break" if variant >= 640 else ""
         return (f"chain_sparse_lds ({prec} CSR chain, weights LDS-resident [tail past ~160 KiB: L2-resident, "
                 f"gathered {8 if (variant % 20) >= 10 else 4} samples ahead with an LDS feature-tag correction]{brk})")
-    if 420 <= variant < 430:
+    if 420 <= variant < 430 or 460 <= variant < 470:
+        brk = ", per-sample isConverged break" if variant >= 460 else ""
         return ("chain_sparse64 (fp64 CSR chain, weights as double vectors in HBM, alpha-scaled SquaredL2, "
-                "one gather round trip per sample)")
+                f"one gather round trip per sample{brk})")
     if 410 <= variant < 420:
         return ("chain_sparse_spec (fp32 CSR chain, weights L2/MALL-resident, gathers 8 samples "
                 "ahead with an LDS feature-tag correction)")
-    if 400 <= variant < 410:
-        return "chain_sparse (fp32 CSR chain, weights L2/MALL-resident, one gather round trip per sample)"
+    if 400 <= variant < 410 or 440 <= variant < 450:
+        brk = ", per-sample isConverged break" if variant >= 440 else ""
+        return f"chain_sparse (fp32 CSR chain, weights L2/MALL-resident, one gather round trip per sample{brk})"
     if 100 <= variant < 200:
         return f"chain_dense (NV={variant - 100}: per-sample chain)"
     return f"chain_general (variant {variant})"

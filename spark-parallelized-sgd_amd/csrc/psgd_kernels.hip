@@ -955,8 +955,8 @@ int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int stora
     if (kp.n_chains <= 0) return 0;
     if (kp.nc > 0)   // LogisticGradient(numClasses > 2)
         return launch_multinomial_chains(L, kp, layout, storage, updater, check_conv, stream, kernel_variant);
-    // PSGD_PER_SAMPLE=1 keeps the per-sample kernels (A/B measurements)
-    static const bool per_sample = [] {
+    // PSGD_PER_SAMPLE=1 keeps the per-sample kernels (A/B measurements, tests; read at every launch)
+    const bool per_sample = [] {
         const char* e = getenv("PSGD_PER_SAMPLE");
         return e && *e && *e != '0';
     }();

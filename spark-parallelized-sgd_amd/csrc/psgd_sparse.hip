@@ -21,6 +21,10 @@
 // adds c x_j / alpha to v_j (the alpha-scaled lazy form). regVal needs ||w|| after
 // the chain's last sample only (PSGD.scala:257): 0.5 * lambda * alpha^2 * ||v||^2.
 // No MFMA, no LDS: the work per sample is a 94-long gather-dot and scatter.
+// The per-sample break (tol > 0, CONV; PSGD.scala:262, :324-336), here and in chain_sparse64: the
+// wave tests isConverged after every sample from z, q = x . x (a second wave sum), c and an f64
+// ||w||^2 recurrence from ||w_in||^2 (L.wnsq0), as chain_sparse_lds does (its header), and leaves
+// the walk after the first passing sample.
 #include "psgd_device.h"
 
 #include <stdlib.h>
@@ -28,7 +32,17 @@
 
 namespace psgd {
 
-template <typename S, int GRAD, int UPD>
+// isConverged(w, w') with w' = a w + c x from z = x . w, q = x . x and nsq = ||w||^2 (updated to
+// ||w'||^2): D < tol^2 max(N, 1) with N = a (a nsq + 2 c z) + c^2 q, D = b (b nsq - 2 c z) + c^2 q
+__device__ __forceinline__ bool conv_step(double a, double c, double z, double q, double tol2, double& nsq) {
+    const double b = 1.0 - a, cq = c * c * q;
+    const double nn = a * __builtin_fma(a, nsq, 2.0 * c * z) + cq;
+    const double dd = b * __builtin_fma(b, nsq, -2.0 * c * z) + cq;
+    nsq = nn > 0.0 ? nn : 0.0;
+    return dd < tol2 * (nn > 1.0 ? nn : 1.0);
+}
+
+template <typename S, int GRAD, int UPD, bool CONV = false>
 __global__ __launch_bounds__(64) void chain_sparse(ChainLaunch L, KParams kp) {
     constexpr bool L2 = UPD == U_SQUARED_L2;
     const int lane = threadIdx.x;
@@ -49,6 +63,8 @@ __global__ __launch_bounds__(64) void chain_sparse(ChainLaunch L, KParams kp) {
     double loss_sum = 0.0;
     float loss_blk = 0.0f;
     int64_t count = 0;
+    double wn = CONV ? *L.wnsq0 : 0.0;   // CONV: ||w||^2
+    const double tol2 = kp.tol * kp.tol;
 
     // Software pipeline: row t+2's entry range is loaded during sample t, row t+1's entries,
     // label and step during sample t (their range is known by then), so the only round trip a
@@ -99,11 +115,16 @@ __global__ __launch_bounds__(64) void chain_sparse(ChainLaunch L, KParams kp) {
 
         float acc = x0 * w0;
         acc = __builtin_fmaf(x1, w1, acc);
+        [[maybe_unused]] float qa = CONV ? __builtin_fmaf(x1, x1, x0 * x0) : 0.0f;
         // entries past the first 128 (rows wider than two per lane)
-        for (int64_t k = kb + 128 + lane; k < ke; k += 64)
-            acc = __builtin_fmaf(float(X[k]), __hip_atomic_load(&V[COL[k]], __ATOMIC_RELAXED,
-                                                                __HIP_MEMORY_SCOPE_AGENT), acc);
+        for (int64_t k = kb + 128 + lane; k < ke; k += 64) {
+            const float xk = float(X[k]);
+            acc = __builtin_fmaf(xk, __hip_atomic_load(&V[COL[k]], __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT), acc);
+            if constexpr (CONV) qa = __builtin_fmaf(xk, xk, qa);
+        }
         float z = wave_sum_uniform(acc);
+        [[maybe_unused]] const float qx = CONV ? wave_sum_uniform(qa) : 0.0f;
         const float sf = float(s);
         if constexpr (L2) {
             // w <- a w + c x: alpha absorbs a; the dot was taken against w = alpha v
@@ -112,6 +133,9 @@ __global__ __launch_bounds__(64) void chain_sparse(ChainLaunch L, KParams kp) {
         }
         float loss;
         const float c = sparse_coef<GRAD>(z, float(y), sf, loss);
+        bool conv = false;
+        if constexpr (CONV)
+            conv = conv_step(L2 ? 1.0 - s * kp.reg : 1.0, double(c), double(z), double(qx), tol2, wn);
         loss_blk += loss;
         if ((t & 31) == 31) { loss_sum += double(loss_blk); loss_blk = 0.0f; }
         count += 1;
@@ -129,6 +153,7 @@ __global__ __launch_bounds__(64) void chain_sparse(ChainLaunch L, KParams kp) {
                 if constexpr (L2) dnsq += nsq_delta(wj, nj);
             }
         }
+        if (conv) break;   // CONV: sample t passed isConverged (it is taken)
         kb = kb1; ke = ke1; kb1 = kb2; ke1 = ke2;
         y = ny; s = ns; c0 = n0; c1 = n1; x0 = nx0; x1 = nx1;
     }
@@ -158,7 +183,7 @@ __global__ __launch_bounds__(64) void chain_sparse(ChainLaunch L, KParams kp) {
 //     lane order; the fold reads w = alpha v straight from the vectors (fold_f64_kernel).
 // Everything but the dot's wave tree is chain_general's arithmetic operator for operator.
 // ------------------------------------------------------------------------------------------
-template <typename S, int GRAD, int UPD>
+template <typename S, int GRAD, int UPD, bool CONV = false>
 __global__ __launch_bounds__(64) void chain_sparse64(ChainLaunch L, KParams kp) {
     constexpr bool L2 = UPD == U_SQUARED_L2;
     const int lane = threadIdx.x;
@@ -183,6 +208,8 @@ __global__ __launch_bounds__(64) void chain_sparse64(ChainLaunch L, KParams kp) 
     double alpha = 1.0;      // SquaredL2: w = alpha * v
     double loss_sum = 0.0;
     int64_t count = 0;
+    double wn = CONV ? *L.wnsq0 : 0.0;   // CONV: ||w||^2
+    const double tol2 = kp.tol * kp.tol;
 
     // software pipeline as chain_sparse: row t+1's entries, label and step and row t+2's range
     // load under row t's gather
@@ -228,13 +255,26 @@ __global__ __launch_bounds__(64) void chain_sparse64(ChainLaunch L, KParams kp) 
         // dot(x, v): chain_general's per-lane fma order over entries lane, lane + 64, lane + 128, ...
         double acc = m_fma(x0, w0, 0.0);
         acc = m_fma(x1, w1, acc);
-        for (int64_t k = kb + 128 + lane; k < ke; k += 64) acc = m_fma(double(X[k]), gather(COL[k]), acc);
-        double z = wave_sum(acc);
+        [[maybe_unused]] double qa = CONV ? m_fma(x1, x1, x0 * x0) : 0.0;
+        for (int64_t k = kb + 128 + lane; k < ke; k += 64) {
+            const double xk = double(X[k]);
+            acc = m_fma(xk, gather(COL[k]), acc);
+            if constexpr (CONV) qa = m_fma(xk, xk, qa);
+        }
+        double z;
+        if constexpr (CONV) {
+            wave_sum2(acc, qa);
+            z = acc;
+        } else {
+            z = wave_sum(acc);
+        }
         if constexpr (L2) z = alpha * z;      // dot(x, w) with w = alpha v
         double mult;
         loss_sum += gradient_scalar<GRAD, double>(z, y, mult);
         count += 1;
         const double a = -s;
+        bool conv = false;
+        if constexpr (CONV) conv = conv_step(L2 ? 1.0 - s * kp.reg : 1.0, a * mult, z, qa, tol2, wn);
         if constexpr (L2) alpha = alpha * (1.0 - s * kp.reg);
         if (mult != 0.0) {
             // v_j + (a * (mult * x_j)) [/ alpha] at the row's indices
@@ -249,6 +289,7 @@ __global__ __launch_bounds__(64) void chain_sparse64(ChainLaunch L, KParams kp) 
                 VW[j] = gather(j) + u;
             }
         }
+        if (conv) break;   // CONV: sample t passed isConverged (it is taken)
         kb = kb1; ke = ke1; kb1 = kb2; ke1 = ke2;
         y = ny; s = ns; c0 = n0; c1 = n1; x0 = nx0; x1 = nx1;
     }
@@ -623,8 +664,7 @@ size_t spec_lds_bytes(int d) {
     return sizeof(SpecHeader) + SR * sizeof(SpecSlot) + (((size_t)d * 2 + 15) / 16) * 16;
 }
 
-// any tol: with the per-sample break (tol > 0) only chain_sparse_lds applies (launch_sparse_chains
-// returns -3 otherwise and the caller falls through to chain_general)
+// any tol: with the per-sample break (tol > 0) chain_sparse_lds or chain_sparse runs it
 bool sparse_path_applies(int layout, int compute, int updater, bool check_conv) {
     (void)check_conv;
     return layout == kCsr && compute == 1 && (updater == U_SIMPLE || updater == U_SQUARED_L2);
@@ -632,10 +672,11 @@ bool sparse_path_applies(int layout, int compute, int updater, bool check_conv) 
 
 template <typename S, int GRAD>
 static int sparse_upd(const ChainLaunch& L, const KParams& kp, int upd, hipStream_t st) {
-    if (upd == U_SIMPLE)
-        hipLaunchKernelGGL((chain_sparse<S, GRAD, U_SIMPLE>), dim3(kp.n_chains), dim3(64), 0, st, L, kp);
-    else
-        hipLaunchKernelGGL((chain_sparse<S, GRAD, U_SQUARED_L2>), dim3(kp.n_chains), dim3(64), 0, st, L, kp);
+    const bool conv = kp.tol > 0.0;   // the per-sample break: instances of their own
+    auto k = upd == U_SIMPLE ? (conv ? chain_sparse<S, GRAD, U_SIMPLE, true> : chain_sparse<S, GRAD, U_SIMPLE, false>)
+                             : (conv ? chain_sparse<S, GRAD, U_SQUARED_L2, true>
+                                     : chain_sparse<S, GRAD, U_SQUARED_L2, false>);
+    hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(64), 0, st, L, kp);
     return (int)hipGetLastError();
 }
 
@@ -756,16 +797,18 @@ __global__ __launch_bounds__(256) void w64_init_kernel(double* __restrict__ wv, 
 }
 
 bool sparse64_path_applies(int layout, int compute, int updater, bool check_conv, bool alpha_ok) {
-    return layout == kCsr && compute == 0 && !check_conv &&
+    (void)check_conv;   // any tol: the per-sample break is a CONV instance (kp.tol > 0)
+    return layout == kCsr && compute == 0 &&
            (updater == U_SIMPLE || (updater == U_SQUARED_L2 && alpha_ok));
 }
 
 template <typename S, int GRAD>
 static int sparse64_upd(const ChainLaunch& L, const KParams& kp, int upd, hipStream_t st) {
-    if (upd == U_SIMPLE)
-        hipLaunchKernelGGL((chain_sparse64<S, GRAD, U_SIMPLE>), dim3(kp.n_chains), dim3(64), 0, st, L, kp);
-    else
-        hipLaunchKernelGGL((chain_sparse64<S, GRAD, U_SQUARED_L2>), dim3(kp.n_chains), dim3(64), 0, st, L, kp);
+    const bool conv = kp.tol > 0.0;   // the per-sample break: instances of their own
+    auto k = upd == U_SIMPLE ? (conv ? chain_sparse64<S, GRAD, U_SIMPLE, true> : chain_sparse64<S, GRAD, U_SIMPLE, false>)
+                             : (conv ? chain_sparse64<S, GRAD, U_SQUARED_L2, true>
+                                     : chain_sparse64<S, GRAD, U_SQUARED_L2, false>);
+    hipLaunchKernelGGL(k, dim3(kp.n_chains), dim3(64), 0, st, L, kp);
     return (int)hipGetLastError();
 }
 
@@ -793,7 +836,14 @@ int launch_sparse64_chains(const ChainLaunch& L, const KParams& kp, int storage,
     by = (kp.n_chains + per - 1) / per;
     hipLaunchKernelGGL(w64_init_kernel, dim3(bx, by), dim3(256), 0, stream, reinterpret_cast<double*>(L.wf32),
                        L.wstride / 2, L.w_in, kp.d, kp.n_chains, per);
-    if (kernel_variant) *kernel_variant = 420 + storage;
+    if (kp.tol > 0.0) {
+        // ||w_in||^2 for the per-sample break's norm recurrence
+        if (!L.wnsq0) return (int)hipErrorInvalidValue;
+        const int e = launch_wnsq0(L, kp.d, false, stream);
+        if (e) return e;
+    }
+    // variant 420 + 40 (the per-sample break) + storage
+    if (kernel_variant) *kernel_variant = 420 + (kp.tol > 0.0 ? 40 : 0) + storage;
     if (storage == 1) return sparse64_grad<float>(L, kp, gradient, updater, stream);
     return sparse64_grad<double>(L, kp, gradient, updater, stream);
 }
@@ -817,13 +867,12 @@ int launch_sparse_chains(const ChainLaunch& L, const KParams& kp, int storage, i
         rc = launch_sparse_lds_chains(L, kp, storage, gradient, updater, max_nnz, stream, kernel_variant);
         if (rc != -3) return rc;
     }
-    // the HBM-weight fp32 kernels have no per-sample break
-    if (kp.tol > 0.0) return -3;
-    if (!no_spec && max_nnz <= SCAP && spec_lds_bytes<8, 32>(kp.d) <= 160 * 1024) {
+    // chain_sparse_spec has no per-sample break; chain_sparse has (variant 440 + storage)
+    if (!no_spec && kp.tol <= 0.0 && max_nnz <= SCAP && spec_lds_bytes<8, 32>(kp.d) <= 160 * 1024) {
         if (kernel_variant) *kernel_variant = 410 + storage;
         return spec_launch<8, 32>(L, kp, storage, gradient, updater, stream);
     }
-    if (kernel_variant) *kernel_variant = 400 + storage;
+    if (kernel_variant) *kernel_variant = 400 + (kp.tol > 0.0 ? 40 : 0) + storage;
     if (storage == 1) return sparse_grad<float>(L, kp, gradient, updater, stream);
     return sparse_grad<double>(L, kp, gradient, updater, stream);
 }

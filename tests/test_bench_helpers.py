@@ -60,3 +60,6 @@ def test_block64_break_label():
     assert bench.kernel_name(342) == "chain_block (NV=2: blocked fp32 chain, 8-row Gram blocks, per-sample isConverged break)"
     assert bench.kernel_name(661).startswith("chain_sparse_lds (fp64") and bench.kernel_name(661).endswith("break)")
     assert bench.kernel_name(641).startswith("chain_sparse_lds (fp32") and "gathered 4" in bench.kernel_name(641)
+    assert bench.kernel_name(440).endswith("per sample, per-sample isConverged break)")
+    assert bench.kernel_name(461).startswith("chain_sparse64") and bench.kernel_name(461).endswith("break)")
+    assert bench.kernel_name(401).endswith("per sample)") and bench.kernel_name(420).endswith("per sample)")

@@ -365,10 +365,11 @@ def test_sparse_lds_per_sample_break_fp32(pkg, oracle, monkeypatch, grad, upd, h
 
 @pytest.mark.parametrize("compute", ["f32", "f64"])
 @pytest.mark.parametrize("upd", ["simple", "squared_l2"])
-def test_sparse_break_beyond_lds_takes_chain_general(pkg, oracle, monkeypatch, compute, upd):
-    """tol > 0 with d past the LDS kernel's range: the HBM-weight kernels have no per-sample
-    break, so chain_general runs it, carrying ||w||^2 from sample to sample (O(nnz) per sample,
-    SquaredL2 in its lazy alpha-scaled form with the norm recurrence); exact in fp64."""
+def test_sparse_break_beyond_lds(pkg, oracle, monkeypatch, compute, upd):
+    """tol > 0 with d past the LDS kernel's range: the HBM-weight kernels chain_sparse (fp32,
+    variant 440 + storage) and chain_sparse64 (fp64, 460 + storage) run the break from the same
+    norm recurrence; exact in fp64. The per-sample fallback (PSGD_PER_SAMPLE=1: chain_general)
+    carries ||w||^2 from sample to sample (O(nnz)) and gives the same counts."""
     from test_gpu_parity import assert_close
     for k in ("PSGD_SPARSE_KERNEL", "PSGD_SPARSE_SK", "PSGD_SPARSE_LDS_HEAD"):
         monkeypatch.delenv(k, raising=False)
@@ -382,7 +383,7 @@ def test_sparse_break_beyond_lds_takes_chain_general(pkg, oracle, monkeypatch, c
     w, h, counts = pkg.runParallelizedSGD(pkg.PartitionedData(parts), pkg.LogisticGradient(),
                                           getattr(pkg, U[upd])(), 1.0, 2, reg, 1.0, np.zeros(d), 0.1,
                                           compute_dtype=compute, return_chain_counts=True)
-    assert pkg.optimization.get_context(0).last_kernel() == 201
+    assert pkg.optimization.get_context(0).last_kernel() == (440 if compute == "f32" else 460)
     wr, hr, cr = oracle.run(oracle.Matrix(y, row_ptr=rp, col=col, val=val, d=d), offs, "logistic", upd,
                             1.0, 2, reg, np.zeros(d), tol=0.1, n_threads=8)
     assert sum(int(c < s) for it in cr for c, s in zip(it, np.diff(offs))) > 0   # breaks happen
@@ -390,3 +391,10 @@ def test_sparse_break_beyond_lds_takes_chain_general(pkg, oracle, monkeypatch, c
         assert [list(c) for c in counts] == [list(c) for c in cr[: len(counts)]]
         assert_close(w, wr, what="beyond-LDS break weights")
         assert_close(h, hr, what="beyond-LDS break loss")
+        # the per-sample fallback (chain_general, O(nnz) norms) gives the same counts
+        monkeypatch.setenv("PSGD_PER_SAMPLE", "1")
+        w2, h2, c2 = pkg.runParallelizedSGD(pkg.PartitionedData(parts), pkg.LogisticGradient(),
+                                            getattr(pkg, U[upd])(), 1.0, 2, reg, 1.0, np.zeros(d), 0.1,
+                                            compute_dtype=compute, return_chain_counts=True)
+        assert [list(c) for c in c2] == [list(c) for c in cr[: len(c2)]]
+        assert_close(w2, wr, what="chain_general break weights")
