@@ -381,12 +381,12 @@ __global__ __launch_bounds__(64) void chain_general(ChainLaunch L, KParams kp) {
     const gmut<double> SB = L.state ? SA + d : nullptr;
     const gmut<double> SC = (L.state && LAYOUT == kCsr) ? SA + 2 * d : nullptr;
 
-    // CSR rows with Simple / SquaredL2 and the per-sample break: ||w||^2 is carried from sample to
-    // sample (O(nnz) per sample instead of a pass over all d): Simple adds each changed
-    // coordinate's nw^2 - old^2; SquaredL2 (lazy form below) the recurrence of chain_block64,
+    // CSR rows with Simple / SquaredL2 / AdaGrad and the per-sample break: ||w||^2 is carried from
+    // sample to sample (O(nnz) per sample instead of a pass over all d): Simple and AdaGrad (which
+    // change only the row's coordinates) add each changed coordinate's nw^2 - old^2; SquaredL2 (lazy form below) the recurrence of chain_block64,
     // ||w'||^2 = a (a ||w||^2 + 2 c z) + c^2 q, ||w - w'||^2 = b (b ||w||^2 - 2 c z) + c^2 q
     // (a = 1 - s lambda, b = 1 - a, c = -s mult, z = x . w, q = x . x). Starts from ||w_in||^2.
-    constexpr bool NORMS = CONV && LAYOUT == kCsr && (UPD == U_SIMPLE || UPD == U_SQUARED_L2);
+    constexpr bool NORMS = CONV && LAYOUT == kCsr && (UPD == U_SIMPLE || UPD == U_SQUARED_L2 || UPD == U_ADAGRAD);
     double wn = 0.0;
     for (int i = lane; i < d; i += 64) {
         const double v = as_global(L.w_in)[i];
@@ -525,11 +525,11 @@ __global__ __launch_bounds__(64) void chain_general(ChainLaunch L, KParams kp) {
                         const double old = W[i];
                         const double nw = old + a * (g / sqrt(acc2 + 1.0));
                         W[i] = nw;
-                        if constexpr (CONV) { const double df = old - nw; dsq += df * df; }
-                    }
-                    if constexpr (CONV) {
-                        wave_mem_fence();
-                        for (int i = lane; i < d; i += 64) nsq += W[i] * W[i];
+                        if constexpr (CONV) {
+                            const double df = old - nw;
+                            dsq += df * df;
+                            nsq += nw * nw - old * old;   // the change of ||w||^2 (NORMS)
+                        }
                     }
                 } else {  // U_ADAM, UPD.scala:252-285: v and r decay at every coordinate
                     for (int64_t k = kb + lane; k < ke; k += 64) SC[COL[k]] = mult * double(X[k]);

@@ -259,14 +259,17 @@ def test_csr_stateful_updater(pkg, oracle):
     parts = [pkg.CsrPartition(y[a:b], rp[a:b + 1] - rp[a], col[rp[a]:rp[b]], val[rp[a]:rp[b]], d)
              for a, b in zip(offs[:-1], offs[1:])]
     data = pkg.PartitionedData(parts)
-    for upd in ("adagrad", "adam"):
+    # tol > 0: the per-sample break (AdaGrad carries ||w||^2 over the row's coordinates, O(nnz))
+    for upd, tol in (("adagrad", 0.0), ("adam", 0.0), ("adagrad", 0.05), ("adam", 0.05)):
         w, h, counts = pkg.runParallelizedSGD(data, pkg.HingeGradient(), getattr(pkg, U[upd])(), 0.5, 3,
-                                              0.0, 1.0, np.zeros(d), 0.0, return_chain_counts=True)
+                                              0.0, 1.0, np.zeros(d), tol, return_chain_counts=True)
         wr, hr, cr = oracle.run(oracle.Matrix(y, row_ptr=rp, col=col, val=val, d=d), offs, "hinge", upd,
-                                0.5, 3, 0.0, np.zeros(d), tol=0.0)
-        assert [list(map(int, c)) for c in counts] == [list(map(int, c)) for c in cr]
-        assert_close(w, wr, what=upd + " weights")
-        assert_close(h, hr, what=upd + " loss")
+                                0.5, 3, 0.0, np.zeros(d), tol=tol)
+        assert [list(map(int, c)) for c in counts] == [list(map(int, c)) for c in cr], (upd, tol)
+        assert_close(w, wr, what=f"{upd} tol={tol} weights")
+        assert_close(h, hr, what=f"{upd} tol={tol} loss")
+        if tol > 0:
+            assert any(c < s for it in cr for c, s in zip(it, np.diff(offs))), "no chain broke"
 
 
 def alpha_in_range(step, reg, n):
