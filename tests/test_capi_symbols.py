@@ -68,6 +68,7 @@ def test_kernel_selection_limits_on_the_host(pkg):
     SIMPLE, L2, L1 = 0, 1, 2
     assert s64(CSR, F64, SIMPLE, False, False) and s64(CSR, F64, L2, False, True)
     assert not s64(CSR, F64, L2, False, False)   # alpha out of range: chain_general renormalises
-    assert not s64(CSR, F64, SIMPLE, True, True)  # per-sample break: chain_general
+    assert s64(CSR, F64, SIMPLE, True, True)      # the per-sample break runs in chain_sparse64 too
+    assert lds64(47236, 94, 0, True, True, 1000)   # ... and in chain_sparse_lds
     assert not s64(CSR, F32, SIMPLE, False, True) and not s64(DENSE, F64, SIMPLE, False, True)
     assert not s64(CSR, F64, L1, False, True)
