@@ -60,42 +60,54 @@ def pmc_traffic(workload, grad, variant, storage, rows, compute="f32", updater="
         glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_*_pmc.json"))
     if not files or not (100 <= variant < 200 or 300 <= variant < 900):
         return None, None
-    waves = 0
     g = {"logistic": 0, "least_squares": 1, "hinge": 2}[grad]
     u = {"simple": 0, "squared_l2": 1, "l1": 2, "adagrad": 3, "adam": 4}.get(updater)
     if u is None:
         return None, None
     sname = "float" if storage == "f32" else "double"
-    if variant < 200:   # chain_dense<S, T, GRAD, UPD, CONV = false, NV, FULL>
-        cname = "float" if compute == "f32" else "double"
-        prefix = f"psgd::chain_dense<{sname}, {cname}, {g}, {u}, false, {variant - 100},"
-    elif variant >= 800:   # chain_split<S, T, GRAD, UPD, CONV = false, NV, FULL, H>
-        cname = "float" if compute == "f32" else "double"
-        prefix = f"psgd::chain_split<{sname}, {cname}, {g}, {u}, false, {variant % 10},"
-    elif variant >= 700:
-        prefix = f"psgd::chain_block64<{sname}, {g}, {u}, {variant % 10}, "
-        waves = 1 + (variant - 700) // 10
-    elif variant >= 600:
-        tname = "double" if (variant % 100) >= 20 else "float"
-        prefix = f"psgd::chain_sparse_lds<{sname}, {tname}, {g}, {u},"
+    cname = "float" if compute == "f32" else "double"
+    nv = variant % 10
+    # the launched instance's template arguments (psgd_*.hip); a trailing CONV argument (the
+    # per-sample break, round 4) is absent from older summaries and means false there
+    if variant >= 800:     # chain_split<S, T, GRAD, UPD, CONV, NV, FULL, H>
+        kern, want = "chain_split", {0: sname, 1: cname, 2: g, 3: u, 4: "false", 5: nv}
+    elif variant >= 700:   # chain_block64<S, GRAD, UPD, NV, FULL, H[, CONV]>
+        kern = "chain_block64"
+        want = {0: sname, 1: g, 2: u, 3: nv, 5: 1 + (variant - 700) % 40 // 10,
+                6: "true" if variant >= 740 else "false"}
+    elif variant >= 600:   # chain_sparse_lds<S, T, GRAD, UPD, SK, TAIL[, CONV]>
+        kern = "chain_sparse_lds"
+        want = {0: sname, 1: "double" if (variant - 600) % 40 >= 20 else "float", 2: g, 3: u,
+                6: "true" if variant >= 640 else "false"}
     elif variant >= 500:
-        prefix = f"psgd::chain_block64<{sname}, {g}, {u}, {variant - 500},"
-    elif variant >= 420:
-        prefix = f"psgd::chain_sparse64<{sname}, {g}, {u}>"
-    elif variant >= 410:
-        prefix = f"psgd::chain_sparse_spec<{sname}, {g}, {u}"
-    elif variant >= 400:
-        prefix = f"psgd::chain_sparse<{sname}, {g}, {u}>"
-    else:
-        prefix = f"psgd::chain_block<{sname}, {g}, {u}, {variant - 300},"
-    # newest round first (r02 before r01), then the file name
+        return None, None
+    elif 420 <= variant < 430 or 460 <= variant < 470:   # chain_sparse64<S, GRAD, UPD[, CONV]>
+        kern, want = "chain_sparse64", {0: sname, 1: g, 2: u, 3: "true" if variant >= 460 else "false"}
+    elif 410 <= variant < 420:   # chain_sparse_spec<S, GRAD, UPD, SK, SR>
+        kern, want = "chain_sparse_spec", {0: sname, 1: g, 2: u}
+    elif variant >= 400:   # chain_sparse<S, GRAD, UPD[, CONV]>
+        kern, want = "chain_sparse", {0: sname, 1: g, 2: u, 3: "true" if variant >= 440 else "false"}
+    elif variant >= 300:   # chain_block<S, GRAD, UPD, NV, FULL[, CONV]>
+        kern, want = "chain_block", {0: sname, 1: g, 2: u, 3: nv, 5: "true" if variant >= 340 else "false"}
+    else:                  # chain_dense<S, T, GRAD, UPD, CONV = false, NV, FULL>
+        kern, want = "chain_dense", {0: sname, 1: cname, 2: g, 3: u, 4: "false", 5: variant - 100}
+    defaults = {"chain_block64": 7, "chain_sparse_lds": 7, "chain_sparse64": 4, "chain_sparse": 4,
+                "chain_block": 6}
+
+    def matches(name):
+        if not name.startswith(f"psgd::{kern}<") or not name.endswith(">"):
+            return False
+        args = name[len(f"psgd::{kern}<"):-1].split(", ")
+        full = defaults.get(kern)
+        if full and len(args) == full - 1:
+            args.append("false")   # the CONV argument of summaries older than it
+        return all(i < len(args) and args[i] == str(v) for i, v in want.items())
+    # newest round first (r04b before r04 before r03), then the file name
     for path in sorted(files, key=lambda f: os.path.basename(f), reverse=True):
         with open(path) as f:
             summ = json.load(f)
         for name, e in summ.get("kernels", {}).items():
-            if waves and not name.rstrip(">").endswith(f", {waves}"):
-                continue   # chain_block64<S, GRAD, UPD, NV, FULL, H>: the same number of chain waves
-            if name.startswith(prefix) and "hbm_bytes" in e:
+            if matches(name) and "hbm_bytes" in e:
                 # the summary's launch may have processed a different row count (--rows): per row
                 per_row = e["hbm_bytes"] / max(summ.get("rows_per_launch") or rows, 1)
                 return per_row * rows, os.path.relpath(path, ROOT)
