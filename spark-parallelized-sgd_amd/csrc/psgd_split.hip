@@ -27,9 +27,11 @@
 //
 // Rows stream through the LDS ring of chain_dense (ring_loader, one loader wave); compute wave 0
 // hands slots back: when it has every partial of sample t, all waves have read row t + 1.
-// The per-element arithmetic is chain_dense's, operator for operator (this file is compiled with
-// -ffp-contract=off); only the dot is reassociated (per-wave partials, wave trees, the fixed
-// order above), inside the fp64 mode's 1e-9 relative bar. Logistic's multiplier is on every
+// The per-element arithmetic is chain_dense's (this file is compiled with -ffp-contract=off)
+// except that AdaGrad's and Adam's status and weight updates are fused where a multiply feeds an
+// add (v = fma(g, 1 - beta, beta v), accum = fma(g, g, accum), w = fma(-lr', u, w), round 4: one
+// rounding fewer each), and the dot is reassociated (per-wave partials, wave trees, the fixed
+// order above) -- all inside the fp64 mode's 1e-9 relative bar. Logistic's multiplier is on every
 // sample's critical path: fp64 takes chain_block64's short-chain 1/(1 + exp(m)) (within ~2 ulp),
 // fp32 the hardware exp2 / reciprocal (as chain_block); the row losses (log1pExp) are summed
 // after the chain from the stored margins, off the sequential path.
@@ -366,7 +368,6 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
         // the sample's scalars that do not depend on its dot, before the exchange's wait (the spin
         // is a branch: nothing after it is moved above it)
         const T a_s = -s;
-        const bool first = t == 0;
         const T iter = T(t + 1);
         T al = T(0);
         if constexpr (UPD == U_ADAM) {
@@ -439,6 +440,7 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
             // below 1), fix1 is the constant 1 + eps and v / fix1 one multiply by its reciprocal:
             // the same operations as the general path (whose sqrt of 1 is exactly 1), hoisted.
             const T beta = T(kp.beta), gamma = T(kp.gamma);
+            const T2 omb = T2{T(1) - beta, T(1) - beta}, omg = T2{T(1) - gamma, T(1) - gamma};
             T2 vv[E2], rr[E2];
             // The test runs once per lane, on an upper bound of the lane's r values: with gamma in
             // [0, 1] every r is +0 or more (or NaN), and such floats order as their bit patterns,
@@ -457,11 +459,11 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
             };
 #pragma unroll
             for (int e = 0; e < E2; ++e) {
+                // v = beta v + (1 - beta) g, r = gamma r + (1 - gamma) g^2, fused; the status starts at
+                // +0, so the first sample's None branch (v = (1 - beta) g) is the same expression
                 const T2 g = mult * x[e];
-                const T2 sq = g * g;
-                T2 v, r;
-                if (first) { v = g * (T(1) - beta); r = sq * (T(1) - gamma); }
-                else { v = ua[e] * beta + g * (T(1) - beta); r = ub[e] * gamma + sq * (T(1) - gamma); }
+                const T2 v = __builtin_elementwise_fma(g, omb, ua[e] * beta);
+                const T2 r = __builtin_elementwise_fma(g * g, omg, ub[e] * gamma);
                 ua[e] = v;
                 ub[e] = r;
                 vv[e] = v;
@@ -483,17 +485,16 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
                 for (int e = 0; e < E2; ++e) {
                     const T2 old = w[e], v = vv[e], r = rr[e];
                     T2 nw;
+                    // w + (-lr) (v / fix1) as fma((-lr) / fix1, v, w)
                     if constexpr (sizeof(T) == 4) {
                         const T fx = __builtin_amdgcn_sqrtf(T(1) - pow_fast(r.x, iter)) + T(kp.eps);
                         const T fy = __builtin_amdgcn_sqrtf(T(1) - pow_fast(r.y, iter)) + T(kp.eps);
-                        nw.x = old.x + al * (v.x * __builtin_amdgcn_rcpf(fx));
-                        nw.y = old.y + al * (v.y * __builtin_amdgcn_rcpf(fy));
+                        nw = __builtin_elementwise_fma(T2{al * __builtin_amdgcn_rcpf(fx), al * __builtin_amdgcn_rcpf(fy)}, v, old);
                     } else {
                         // sqrt and v / fix1 by the hardware estimates + one Newton step (~1e-14)
                         const T fx = sqrt_newton(one_minus_pow_iter(r.x, iter)) + T(kp.eps);
                         const T fy = sqrt_newton(one_minus_pow_iter(r.y, iter)) + T(kp.eps);
-                        nw.x = old.x + al * (v.x * recip_newton(fx));
-                        nw.y = old.y + al * (v.y * recip_newton(fy));
+                        nw = __builtin_elementwise_fma(T2{al * recip_newton(fx), al * recip_newton(fy)}, v, old);
                     }
                     w[e] = nw;
                     if constexpr (CONV) { const T2 df = old - nw; dsq2 += df * df; nsq2 += nw * nw; }
@@ -502,12 +503,11 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
                 T rfix;
                 if constexpr (sizeof(T) == 4) rfix = __builtin_amdgcn_rcpf(T(1) + T(kp.eps));
                 else rfix = recip_newton(T(1) + T(kp.eps));
+                const T alr = al * rfix;   // the general path's al * (1 / fix1) at fix1 = 1 + eps
 #pragma unroll
                 for (int e = 0; e < E2; ++e) {
                     const T2 old = w[e], v = vv[e];
-                    T2 nw;
-                    nw.x = old.x + al * (v.x * rfix);
-                    nw.y = old.y + al * (v.y * rfix);
+                    const T2 nw = __builtin_elementwise_fma(T2{alr, alr}, v, old);
                     w[e] = nw;
                     if constexpr (CONV) { const T2 df = old - nw; dsq2 += df * df; nsq2 += nw * nw; }
                 }
@@ -522,15 +522,15 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
                     // (the status starts at +0, and +0 + g*g is g*g: the first sample's None
                     // branch without a select)
                     const T2 g = mult * x[e];
-                    const T2 acc2 = ua[e] + g * g;
+                    const T2 acc2 = __builtin_elementwise_fma(g, g, ua[e]);
                     ua[e] = acc2;
+                    T2 q;   // g / sqrt(accum + 1)
                     if constexpr (sizeof(T) == 4) {
-                        nw.x = old.x + a_s * (g.x * __builtin_amdgcn_rsqf(acc2.x + T(1)));
-                        nw.y = old.y + a_s * (g.y * __builtin_amdgcn_rsqf(acc2.y + T(1)));
+                        q = g * T2{__builtin_amdgcn_rsqf(acc2.x + T(1)), __builtin_amdgcn_rsqf(acc2.y + T(1))};
                     } else {
-                        nw.x = old.x + a_s * (g.x * rsqrt_newton(acc2.x + T(1)));
-                        nw.y = old.y + a_s * (g.y * rsqrt_newton(acc2.y + T(1)));
+                        q = g * T2{rsqrt_newton(acc2.x + T(1)), rsqrt_newton(acc2.y + T(1))};
                     }
+                    nw = __builtin_elementwise_fma(T2{a_s, a_s}, q, old);
                 } else if constexpr (UPD == U_SQUARED_L2) {
                     nw = old * l2c;                     // brzWeights :*= (1 - s*lambda) (UPD.scala:172)
                     nw = nw + a_s * (mult * x[e]);      // axpy(-s, grad, w)
