@@ -197,8 +197,9 @@ __device__ __forceinline__ double one_minus_pow_iter(double r, double iter) {
 // 1 / (1 + exp(m)) in f64 with a short dependent chain: the chains evaluate it once per row on
 // their critical path, where the library exp (Horner) and IEEE division (div_scale / div_fmas /
 // div_fixup) are ~30 dependent f64 operations. Here: exp(m) = 2^k e^r, k = rint(m log2 e),
-// r = m - k ln2 (two-part ln2, |r| <= ln2/2), e^r by its Taylor polynomial of degree 13
-// (truncation < 2e-16 relative) evaluated Estrin-style (depth 5 instead of 13), 2^k by ldexp;
+// r = m - k ln2 (two-part ln2, |r| <= ln2/2), e^r by its Taylor polynomial of degree 11
+// (truncation < 1e-14 relative; degree 13 until round 4, two more FMAs on every row's critical
+// path for digits the 1e-9 bar does not use) evaluated Estrin-style (depth 4), 2^k by ldexp;
 // the reciprocal by v_rcp_f64 and one Newton step (above). Within ~1e-14 relative of the
 // reference's 1.0 / (1.0 + exp(margin)) (the fp64 mode's bar is 1e-9 relative). m is clamped to
 // [-746, 709] (exp(-746) is 0 in f64; beyond 709 the result is ~1e-308 instead of 0); a NaN
@@ -216,13 +217,11 @@ __device__ __forceinline__ double recip_one_plus_exp(double m) {
     const double p67 = __builtin_fma(r, 1.0 / 5040, 1.0 / 720);
     const double p89 = __builtin_fma(r, 1.0 / 362880, 1.0 / 40320);
     const double pab = __builtin_fma(r, 1.0 / 39916800, 1.0 / 3628800);
-    const double pcd = __builtin_fma(r, 1.0 / 6227020800.0, 1.0 / 479001600);
     const double q03 = __builtin_fma(r2, p23, p01);
     const double q47 = __builtin_fma(r2, p67, p45);
     const double q8b = __builtin_fma(r2, pab, p89);
     const double q07 = __builtin_fma(r4, q47, q03);
-    const double q8d = __builtin_fma(r4, pcd, q8b);
-    const double er = __builtin_fma(r8, q8d, q07);
+    const double er = __builtin_fma(r8, q8b, q07);
     return recip_newton(1.0 + __builtin_amdgcn_ldexp(er, (int)kd));
 }
 

@@ -443,10 +443,10 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
             const T2 omb = T2{T(1) - beta, T(1) - beta}, omg = T2{T(1) - gamma, T(1) - gamma};
             T2 vv[E2], rr[E2];
             // The test runs once per lane, on an upper bound of the lane's r values: with gamma in
-            // [0, 1] every r is +0 or more (or NaN), and such floats order as their bit patterns,
-            // so the largest pattern with the sign bit cleared is the largest r, or a NaN when any
-            // r is one (fp64: the high words, completed with all-ones low words: a bound >= every
-            // r). The threshold has half a unit of margin over the per-coordinate test below, so
+            // [0, 1] every r is +0 or more, +inf or a NaN, and such floats order as their bit
+            // patterns (a NaN of either sign compares above +inf), so the largest pattern is the
+            // largest r, or a NaN when any r is one (fp64: the high words, completed with all-ones
+            // low words: a bound >= every r). The threshold has half a unit of margin over the per-coordinate test below, so
             // the bound passing implies every coordinate passing (v_log_f32 need not be strictly
             // monotone); gamma outside [0, 1] takes the general path.
             uint32_t rbits = 0;
@@ -454,7 +454,6 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
                 uint32_t b;
                 if constexpr (sizeof(T) == 4) b = __float_as_uint(r);
                 else b = (uint32_t)((uint64_t)__double_as_longlong(r) >> 32);
-                b &= 0x7FFFFFFFu;
                 rbits = b > rbits ? b : rbits;
             };
 #pragma unroll
