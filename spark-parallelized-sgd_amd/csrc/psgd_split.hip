@@ -371,10 +371,19 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
         const T iter = T(t + 1);
         T al = T(0);
         if constexpr (UPD == U_ADAM) {
-            if constexpr (sizeof(T) == 4) al = -(s / (T(1) - pow_fast(T(kp.beta), iter)));
-            // fp64: 1 - beta^iter as 1.0 once beta^iter <= 2^-54 (bit-identical, no library pow
-            // per sample on the chain) and the division by rcp + one Newton step
-            else al = -(s * recip_newton(one_minus_pow_iter(T(kp.beta), iter)));
+            // lr = s / (1 - beta^iter); once 1 - beta^iter is exactly 1.0 (after a few tens of
+            // samples) the quotient is s itself: a wave-uniform branch skips the division
+            // (fp32: IEEE division, ~10 instructions; fp64: rcp + one Newton step, which gives
+            // exactly 1 for 1.0)
+            if constexpr (sizeof(T) == 4) {
+                const T q = T(1) - pow_fast(T(kp.beta), iter);
+                al = q == T(1) ? -s : -(s / q);
+            } else {
+                // 1 - beta^iter as 1.0 once beta^iter <= 2^-54 (bit-identical, no library pow per
+                // sample on the chain)
+                const T q = one_minus_pow_iter(T(kp.beta), iter);
+                al = q == T(1) ? -s : -(s * recip_newton(q));
+            }
         }
         [[maybe_unused]] const T shrink = T(kp.reg) * s;          // L1 (UPD.scala:133)
         [[maybe_unused]] const T l2c = T(1) - s * T(kp.reg);      // SquaredL2 (UPD.scala:169)
