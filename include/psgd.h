@@ -168,9 +168,19 @@ int32_t psgd_convergence_terms_device(psgd_ctx* ctx, int32_t d, const double* d_
 int32_t psgd_initial_regval(psgd_ctx* ctx, const psgd_params* params, int32_t d, const double* w,
                             double* regval_out);
 
-/* Diagnostics: which chain kernel the last epoch launched (101/102/104/108 = register-resident
- * dense kernel with NV 16-byte vectors per lane; 200 = general dense; 201 = general CSR;
- * 301/302/304/308 = blocked fp32 dense kernel with NV 16-byte vectors per lane). */
+/* Diagnostics: which chain kernel the last epoch launched (DESIGN.md §3 has the table):
+ * 100 + NV   per-sample dense chain (chain_dense), NV 16-byte row vectors per lane;
+ * 200 / 201  general dense / CSR chain (chain_general);
+ * 300 + NV   blocked fp32 dense chain (chain_block); 340 + NV with the per-sample break (tol > 0);
+ * 400 / 410 / 420 + storage   fp32 CSR (chain_sparse / chain_sparse_spec), fp64 CSR with HBM
+ *            weights (chain_sparse64); +40 with the per-sample break (440, 460);
+ * 500 + layout  multinomial LogisticGradient (chain_multinomial);
+ * 600 + 10 (SK = 8) + 20 (fp64) + storage   CSR with LDS-resident weights (chain_sparse_lds);
+ *            +40 with the per-sample break;
+ * 700 + 10 (H - 1) + NV   blocked fp64 dense chain (chain_block64, H chain waves); +40 with the
+ *            per-sample break;
+ * 800 + 10 H + NV   per-sample dense chain with features over H waves (chain_split).
+ * storage: 1 = f32 rows, 0 = f64 rows. */
 int32_t psgd_ctx_last_kernel(psgd_ctx* ctx);
 
 /* Diagnostics: device time of the last chain-kernel launch in milliseconds, from HIP events
