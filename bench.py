@@ -8,7 +8,8 @@ in HBM before the timed region. Default workload = BASELINE.json configs[1]
 ("Least-squares linear regression, dense 10M x 512 fp32, 256 chains on 1 MI355X"); per-GPU work
 is fixed as N grows (weak scaling: every GPU runs its own 256 chains x 10M rows).
 
-Prints ONE JSON line (rank 0).
+Prints ONE JSON line (rank 0), kept under LINE_LIMIT bytes; the secondary workloads' full records
+go to --detail (a JSON file), their summary onto the line.
 """
 from __future__ import annotations
 
@@ -174,6 +175,8 @@ def parse():
     ap.add_argument("--tol", type=float, default=0.0,
                     help="convergenceTol of the headline workload (PSGD.scala:262 per-sample break; the "
                          "reference's default is 0.001; BASELINE's configs run 0)")
+    ap.add_argument("--detail", default=os.path.join("gpurun_out", "bench_detail.json"),
+                    help="file for the full secondary records ('' = none); stdout carries a summary")
     ap.add_argument("--prewarm-s", type=float, default=1.0,
                     help="untimed epochs for this long before the warmup steps (GPU clock ramp)")
     return ap.parse_args()
@@ -509,9 +512,9 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
                         if csr else {}),
                      "avg_kernel_ms": avg_kernel_s * 1e3,
                      "avg_epoch_ms": avg_epoch_s * 1e3,
+                     "variant": variant,
                      "timing": "HIP events recorded around each chain-kernel launch on its stream"},
-        "prewarm": {"seconds": prewarm_s, "epochs": prewarm_epochs,
-                    "note": "untimed epochs before the warmup steps (GPU clock ramp); their model is discarded"},
+        "prewarm": {"seconds": prewarm_s, "epochs": prewarm_epochs},   # untimed, model discarded
         "_meta": (grad, d, P, step, csr, upd_name, reg),
     }
     del engine, data, parts, all_parts
@@ -578,8 +581,7 @@ def main():
     # Secondary lines (one GPU only): the other BASELINE configs' per-GPU workloads under the
     # same clock, each with its own roofline (VERDICT r01 "let the driver observe" them).
     secondary = [s for s in args.secondary.split(",") if s] if world == 1 else []
-    if secondary:
-        out["secondary"] = []
+    records = []
     for spec in secondary:
         wl, comp, upd, sto = (spec.split(":") + ["", "", ""])[:4]
         torch.cuda.empty_cache()
@@ -588,26 +590,70 @@ def main():
                              SECONDARY_ROWS.get(wl, 0), 1.0, args.steps, args.warmup,
                              min(args.prewarm_s, 0.5), updater=upd, storage=sto)
         except Exception as e:   # a secondary line never hides the headline
-            out["secondary"].append({"spec": spec, "error": f"{type(e).__name__}: {e}"})
+            records.append({"spec": spec, "error": f"{type(e).__name__}: {e}"})
             continue
         r.pop("_meta")
         r["spec"] = spec
         r["samples_per_s"] = r.pop("value")
         r["loss"] = float(r["loss"])
-        out["secondary"].append(r)
-    if secondary:
-        # the same numbers once more, compact and last on the line: a reader that keeps only
-        # the line's tail still sees every secondary measurement
-        out["secondary_summary"] = [
-            {"spec": r["spec"], "error": r["error"]} if "error" in r else
-            {"spec": r["spec"], "samples_per_s": round(r["samples_per_s"]),
-             "frac": round(r["roofline"]["frac"], 4), "kernel_ms": round(r["roofline"]["avg_kernel_ms"], 3),
-             "B_per_sample": r["roofline"]["bytes_per_sample"]}
-            for r in out["secondary"]]
+        records.append(r)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        if records:
+            out["secondary_detail"] = write_detail(args.detail, out, records)
+        print(final_line(out, records), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+# The driver keeps only the tail of stdout (about 8 KB, stderr appended after it) and parses the
+# last line: round 4's line carried 14 full secondary records (21.7 KB) and was not parsed.
+LINE_LIMIT = 6000
+
+
+def secondary_summary(records):
+    """One compact entry per secondary workload: what the driver's line carries."""
+    return [{"spec": r["spec"], "error": r["error"][:200]} if "error" in r else
+            {"spec": r["spec"], "samples_per_s": round(r["samples_per_s"]),
+             "frac": round(r["roofline"]["frac"], 4), "kernel_ms": round(r["roofline"]["avg_kernel_ms"], 3),
+             "B_per_sample": r["roofline"]["bytes_per_sample"],
+             "variant": r["roofline"].get("variant")}
+            for r in records]
+
+
+def write_detail(path, out, records):
+    """The full secondary records (config, roofline, prewarm of each) go to a JSON file, not to
+    the stdout line. Returns the path written, or None when it could not be written."""
+    if not path:
+        return None
+    try:
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump({"headline": out, "secondary": records}, f, indent=1)
+        return os.path.relpath(os.path.abspath(path), ROOT)
+    except OSError:
+        return None
+
+
+def final_line(out, records):
+    """The ONE stdout JSON line: headline fields, roofline, cpu baselines and the compact
+    secondary summary. Never longer than LINE_LIMIT bytes: if it would be, the roofline's and
+    the cpu baselines' descriptive strings are dropped first, then the summary's extra fields."""
+    line = dict(out)
+    if records:
+        line["secondary_summary"] = secondary_summary(records)
+    s = json.dumps(line, separators=(",", ":"))
+    if len(s) > LINE_LIMIT:
+        for k in ("cpu_baseline", "cpu_baseline_c1"):
+            if k in line:
+                line[k] = {kk: v for kk, v in line[k].items() if kk != "sample"}
+        line["roofline"] = {k: v for k, v in line["roofline"].items() if k not in ("kernel", "timing")}
+        line["config"] = {k: v for k, v in line["config"].items() if k != "parallelism"}
+        s = json.dumps(line, separators=(",", ":"))
+    if len(s) > LINE_LIMIT and records:
+        line["secondary_summary"] = [{k: v for k, v in e.items() if k in ("spec", "samples_per_s", "frac")}
+                                     for e in line["secondary_summary"]]
+        s = json.dumps(line, separators=(",", ":"))
+    return s
 
 
 if __name__ == "__main__":

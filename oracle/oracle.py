@@ -59,6 +59,9 @@ def lib():
                                     C.POINTER(_Params), dp, dp, dp, dp, i64p, C.c_int32]
         L.or_chain.argtypes = [C.POINTER(_Matrix), C.c_int64, C.c_int64, C.POINTER(_Params),
                                dp, dp, dp, dp, i64p]
+        L.or_set_margin_probe.argtypes = [dp, C.c_int32, C.c_int32]
+        L.or_set_ratio_trace.argtypes = [C.c_int32, dp, C.c_int64]
+        L.or_ratio_trace_len.restype = C.c_int64
         L.or_fdlibm_log.argtypes = [C.c_double]
         L.or_fdlibm_log.restype = C.c_double
         L.or_generate_gd_input.argtypes = [C.c_double, C.c_double, C.c_int32, C.c_int32, dp, dp]
@@ -150,6 +153,44 @@ def run(mat: Matrix, part_offsets, gradient, updater, step, iters, reg, w0, tol=
         raise RuntimeError("oracle or_run failed")
     n = nh.value
     return w_out, hist[:n].copy(), counts[:iters].copy()
+
+
+# Break margins: the kernels decide isConverged with other (reassociated,
+# recurrence-carried) arithmetic than the reference's sums, so an exact per-chain count is a
+# guarantee only where the oracle's decision is far from flipping. Not thread-safe (one global
+# probe in the C library); test infrastructure only.
+BREAK_MARGIN_F64 = 1e-11   # the fp64 kernels' stated bound on the relative error of diff / rhs
+
+
+def run_with_margins(mat: Matrix, part_offsets, gradient, updater, step, iters, reg, w0, tol=0.001,
+                     **kw):
+    """run() plus margins[iters_run, P]: per outer iteration and chain, the smallest
+    |diff / (tol max(norm, 1)) - 1| over the chain's per-sample isConverged tests
+    (ParallelizedSGD.scala:262, :324-336) -- how far the closest decision was from flipping
+    (+inf for a chain that tested nothing)."""
+    P = len(part_offsets) - 1
+    buf = np.full((max(iters, 1), max(P, 1)), np.inf)
+    lib().or_set_margin_probe(_dp(buf), max(iters, 1), max(P, 1))
+    try:
+        w, h, counts = run(mat, part_offsets, gradient, updater, step, iters, reg, w0, tol=tol, **kw)
+    finally:
+        lib().or_set_margin_probe(None, 0, 0)
+    return w, h, counts, buf[: len(counts)].copy()
+
+
+def ratio_trace(mat: Matrix, part_offsets, chain, gradient, updater, step, reg, w0, **kw):
+    """r_k = diff_k / max(norm_k, 1) of every sample k of `chain` in the first outer iteration at
+    tol = 0 (no break): sample k passes isConverged iff r_k < tol, so tol = r_k (1 +- e) puts a
+    decision e from flipping (the adversarial break cases)."""
+    n = int(part_offsets[chain + 1] - part_offsets[chain])
+    buf = np.zeros(max(n, 1))
+    lib().or_set_ratio_trace(chain, _dp(buf), n)
+    try:
+        run(mat, part_offsets, gradient, updater, step, 1, reg, w0, tol=0.0, **kw)
+        m = lib().or_ratio_trace_len()
+    finally:
+        lib().or_set_ratio_trace(-1, None, 0)
+    return buf[:m].copy()
 
 
 def run_chains(mat: Matrix, part_offsets, gradient, updater, step, reg, w_in, tol=0.0,

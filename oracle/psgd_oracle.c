@@ -76,6 +76,55 @@ int or_is_converged(int32_t d, const double* prev, const double* cur, double tol
 }
 
 /* ------------------------------------------------------------------------------------------
+ * Break-margin probe (test infrastructure only). isConverged decides
+ * `diff < tol * max(norm, 1)`; the decision flips only if `rho = diff / (tol * max(norm, 1))`
+ * crosses 1. When a probe is set, every per-sample test of chain p in outer iteration i (1-based;
+ * 1 for or_run_chains) lowers g_margin[(i - 1) * P + p] to |rho - 1|, the relative distance of that
+ * decision from flipping; and every sample of chain g_trace_chain in iteration 1 appends the
+ * tol-free r = diff / max(norm, 1) to g_trace. The decisions themselves are unchanged.
+ * ------------------------------------------------------------------------------------------ */
+static double* g_margin = NULL;
+static int32_t g_margin_iters = 0, g_margin_P = 0, g_iter = 1;
+static double* g_trace = NULL;
+static int64_t g_trace_cap = 0, g_trace_n = 0;
+static int32_t g_trace_chain = -1;
+
+void or_set_margin_probe(double* buf, int32_t iters, int32_t P) {
+    g_margin = buf;
+    g_margin_iters = iters;
+    g_margin_P = P;
+}
+
+void or_set_ratio_trace(int32_t chain, double* buf, int64_t cap) {
+    g_trace_chain = buf ? chain : -1;
+    g_trace = buf;
+    g_trace_cap = cap;
+    g_trace_n = 0;
+}
+
+int64_t or_ratio_trace_len(void) { return g_trace_n; }
+
+/* or_is_converged with the probe's bookkeeping for chain p (p < 0: none) */
+static int is_converged_probed(int32_t d, const double* prev, const double* cur, double tol, int32_t p) {
+    if (p < 0 || (!g_margin && !(g_trace && p == g_trace_chain && g_iter == 1)))
+        return or_is_converged(d, prev, cur, tol);
+    double s = 0.0;
+    for (int32_t i = 0; i < d; ++i) {
+        double t = prev[i] - cur[i];
+        s = s + t * t;
+    }
+    const double diff = sqrt(s), den = jmax(norm2(d, cur), 1.0), rhs = tol * den;
+    const int conv = diff < rhs;
+    if (g_margin && p < g_margin_P && g_iter >= 1 && g_iter <= g_margin_iters && rhs > 0.0) {
+        double* m = &g_margin[(size_t)(g_iter - 1) * (size_t)g_margin_P + (size_t)p];
+        const double dist = fabs(diff / rhs - 1.0);
+        if (dist < *m) *m = dist;
+    }
+    if (g_trace && p == g_trace_chain && g_iter == 1 && g_trace_n < g_trace_cap) g_trace[g_trace_n++] = diff / den;
+    return conv;
+}
+
+/* ------------------------------------------------------------------------------------------
  * Per-sample gradient, one row.  A gradient is either dense (g[d] valid) or sparse over the
  * row's own index set (gv[k] for idx[k]); an "empty sparse" gradient has nnz == 0.
  * ------------------------------------------------------------------------------------------ */
@@ -340,7 +389,7 @@ double or_initial_regval(int32_t d, const double* w, const or_params* prm) {
  * partition's sampled subsequence in iterator order) when rows is not null. */
 static int chain_rows(const or_matrix* m, int64_t r0, int64_t r1, const int32_t* rows,
                       const or_params* prm, const double* w_in, double* w_out, double* rv_out,
-                      double* loss_out, int64_t* count_out) {
+                      double* loss_out, int64_t* count_out, int32_t p) {
     const int32_t d = or_weight_dim(m->d, prm);   /* weights; rows have m->d features */
     const int32_t K = prm->gradient == OR_GRAD_LOGISTIC && prm->num_classes > 2 ? prm->num_classes : 0;
     size_t nd = (size_t)(d > 0 ? d : 1);
@@ -391,7 +440,7 @@ static int chain_rows(const or_matrix* m, int64_t r0, int64_t r1, const int32_t*
         localLossSum += loss;
         count += 1;
         j += 1;
-        if (or_is_converged(d, old, w, prm->convergence_tol)) break;
+        if (is_converged_probed(d, old, w, prm->convergence_tol, p)) break;
         memcpy(old, w, sizeof(double) * (size_t)d);
     }
     memcpy(w_out, w, sizeof(double) * (size_t)d);
@@ -405,7 +454,7 @@ static int chain_rows(const or_matrix* m, int64_t r0, int64_t r1, const int32_t*
 int or_chain(const or_matrix* m, int64_t r0, int64_t r1, const or_params* prm,
              const double* w_in, double* w_out, double* rv_out, double* loss_out,
              int64_t* count_out) {
-    return chain_rows(m, r0, r1, NULL, prm, w_in, w_out, rv_out, loss_out, count_out);
+    return chain_rows(m, r0, r1, NULL, prm, w_in, w_out, rv_out, loss_out, count_out, -1);
 }
 
 /* ------------------------------------------------------------------------------------------
@@ -453,7 +502,7 @@ static void* chain_worker(void* arg) {
         }
         if (jb->limits && r1 - r0 > jb->limits[p]) r1 = r0 + jb->limits[p];
         if (chain_rows(jb->m, r0, r1, rows, jb->prm, jb->w_in, jb->w_out + (size_t)p * (size_t)d,
-                       &jb->rv[p], &jb->loss[p], &jb->cnt[p]) != 0)
+                       &jb->rv[p], &jb->loss[p], &jb->cnt[p], p) != 0)
             jb->rc = -1;
     }
     return NULL;
@@ -489,6 +538,7 @@ int or_run_chains(const or_matrix* m, int32_t P, const int64_t* part_offsets,
                   const int64_t* part_limits, const or_params* prm, const double* w_in,
                   double* w_out, double* rv_out, double* loss_out, int64_t* count_out,
                   int32_t n_threads) {
+    g_iter = 1;
     return run_chains(m, P, part_offsets, part_limits, NULL, NULL, prm, w_in, w_out, rv_out,
                       loss_out, count_out, n_threads);
 }
@@ -552,6 +602,7 @@ int or_run(const or_matrix* m, int32_t P, const int64_t* part_offsets,
                 for (int64_t k = 0; k < nrows[p]; ++k) rows[p][k] += (int32_t)r0;
             }
         }
+        g_iter = i;   /* the break-margin probe's row */
         rc = run_chains(m, P, part_offsets, NULL, rows, nrows, prm, weights, cw, crv, closs, ccnt,
                         n_threads);
         if (rc) break;

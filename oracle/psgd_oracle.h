@@ -102,6 +102,14 @@ int or_run_chains(const or_matrix* m, int32_t P, const int64_t* part_offsets,
                   double* w_out /*[P*d]*/, double* rv_out, double* loss_out, int64_t* count_out,
                   int32_t n_threads);
 
+/* Break-margin probe (test infrastructure): buf[iters * P], initialised by the caller (e.g. to
+ * +inf), receives per (outer iteration, chain) the smallest |diff / (tol max(norm, 1)) - 1| over
+ * the chain's isConverged tests; NULL turns it off. or_set_ratio_trace records, for one chain of
+ * the first iteration, r = diff / max(norm, 1) of every sample (up to cap values). */
+void or_set_margin_probe(double* buf, int32_t iters, int32_t P);
+void or_set_ratio_trace(int32_t chain, double* buf, int64_t cap);
+int64_t or_ratio_trace_len(void);
+
 /* RDD.sample(false, fraction, seed) [ext Spark 1.6.1]: the per-partition seeds
  * (java.util.Random(seed).nextLong() in partition order), XORShiftRandom.hashSeed, and the
  * BernoulliSampler's row selection for one partition of n rows (returns the count, writes the

@@ -245,7 +245,7 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
     constexpr int kRoleLoader = H == 1 ? 1 : 4;
     constexpr int GSZ = gram_slot64<CONV>();
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    // LDS: [RingHeader 16 B][GramHeader64 16 B][XchgHeader64 16 B][exchange 34 doubles]
+    // LDS: [RingHeader 16 B][GramHeader64 16 B][XchgHeader64 32 B][exchange 36 doubles]
     //      [meta ring MB x 256 B][Gram ring GS x GSZ doubles][row ring R x ROW_BYTES]
     RingHeader* hdr = reinterpret_cast<RingHeader*>(smem);
     GramHeader64* ghdr = reinterpret_cast<GramHeader64*>(smem + sizeof(RingHeader));

@@ -994,18 +994,27 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         L.walpha = ctx->walpha.as<double>();
         L.wnsq0 = ctx->wnsq0.as<double>();
     }
-    if (layout == psgd::kCsr && params->compute_dtype == PSGD_F64 && !mn &&
-        (psgd::sparse_lds64_applies(d, max_nnz, params->updater, conv, true, n_max) ||
-         psgd::sparse64_path_applies(layout, 0, params->updater, conv, true))) {
+    // SquaredL2's alpha-scaled CSR kernels need every prefix product of (1 - s_j lambda) in range
+    const bool alpha_ok = params->updater != PSGD_UPDATER_SQUARED_L2 ||
+                          alpha_in_range(ctx, params->step_size, params->reg_param, n_max);
+    if (layout == psgd::kCsr && params->compute_dtype == PSGD_F64 && !mn && !psgd::per_sample_forced() &&
+        (psgd::sparse_lds64_applies(d, max_nnz, params->updater, conv, alpha_ok, n_max) ||
+         psgd::sparse64_path_applies(layout, 0, params->updater, conv, alpha_ok))) {
         // the fp64 CSR kernels' per-chain f64 vectors (d + 1152 doubles, in L.wf32's memory),
-        // chain_sparse64's alphas, and ||w_in||^2 for the per-sample break
-        L.wstride = 2 * (((int64_t)d + 128 + 1024 + 63) / 64 * 64);
-        HIP_TRY(ctx->wf32.ensure((size_t)P * (size_t)L.wstride * sizeof(float)));
-        HIP_TRY(ctx->walpha.ensure((size_t)P * sizeof(double)));
-        HIP_TRY(ctx->wnsq0.ensure(sizeof(double)));
-        L.wf32 = ctx->wf32.as<float>();
-        L.walpha = ctx->walpha.as<double>();
-        L.wnsq0 = ctx->wnsq0.as<double>();
+        // chain_sparse64's alphas, and ||w_in||^2 for the per-sample break. Only when one of those
+        // kernels will run (chain_general keeps its weights in w_out, and C5's
+        // vectors are ~34 GB); if HBM cannot hold them the epoch runs chain_general instead.
+        const int64_t stride = 2 * (((int64_t)d + 128 + 1024 + 63) / 64 * 64);
+        if (ctx->wf32.ensure((size_t)P * (size_t)stride * sizeof(float)) == hipSuccess) {
+            HIP_TRY(ctx->walpha.ensure((size_t)P * sizeof(double)));
+            HIP_TRY(ctx->wnsq0.ensure(sizeof(double)));
+            L.wstride = stride;
+            L.wf32 = ctx->wf32.as<float>();
+            L.walpha = ctx->walpha.as<double>();
+            L.wnsq0 = ctx->wnsq0.as<double>();
+        } else {
+            (void)hipGetLastError();   // the failed allocation is not the epoch's error
+        }
     }
     if (params->gradient == PSGD_GRADIENT_LOGISTIC && params->compute_dtype == PSGD_F32 &&
         layout == psgd::kDense) {
@@ -1032,8 +1041,7 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
     kp.n_chains = P;
     kp.nc = mn ? params->num_classes - 1 : 0;
     kp.n_max = n_max;
-    kp.alpha_ok = params->updater != PSGD_UPDATER_SQUARED_L2 ||
-                  alpha_in_range(ctx, params->step_size, params->reg_param, n_max);
+    kp.alpha_ok = alpha_ok;
 
     int weights_in = psgd::kWeightsOut;   // where the launch left the chains' weights
     if (sample_empty) {

@@ -125,6 +125,8 @@ int launch_wnsq0(const ChainLaunch& L, int d, bool round_f32, hipStream_t st);
 // SquaredL2 when kp.alpha_ok; the chain's double vector lives in its slice of L.wf32 (>= 2 (d +
 // 1152) floats), its alpha in L.walpha; weights end there (w = walpha v, launch_fold_f64).
 bool sparse64_path_applies(int layout, int compute, int updater, bool check_conv, bool alpha_ok);
+// PSGD_PER_SAMPLE=1 (tests, A/B): launch_chains keeps the per-sample kernels
+bool per_sample_forced();
 int launch_sparse64_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
                            int updater, hipStream_t stream, int* kernel_variant);
 // The combiner over chain_sparse64's vectors: w_p = walpha[p] * v_p[i] (v_p doubles).

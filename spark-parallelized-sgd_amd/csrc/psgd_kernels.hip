@@ -947,6 +947,12 @@ static int dispatch_grad(const ChainLaunch& L, const KParams& kp, int layout, in
     }
 }
 
+// PSGD_PER_SAMPLE=1 keeps the per-sample kernels (A/B measurements, tests; read at every launch)
+bool per_sample_forced() {
+    const char* e = getenv("PSGD_PER_SAMPLE");
+    return e && *e && *e != '0';
+}
+
 int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int storage, int compute,
                   int gradient, int updater, bool check_conv, int64_t min_ld, int64_t max_ld,
                   int lds_spread, hipStream_t stream, int* kernel_variant, int64_t max_nnz,
@@ -955,11 +961,7 @@ int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int stora
     if (kp.n_chains <= 0) return 0;
     if (kp.nc > 0)   // LogisticGradient(numClasses > 2)
         return launch_multinomial_chains(L, kp, layout, storage, updater, check_conv, stream, kernel_variant);
-    // PSGD_PER_SAMPLE=1 keeps the per-sample kernels (A/B measurements, tests; read at every launch)
-    const bool per_sample = [] {
-        const char* e = getenv("PSGD_PER_SAMPLE");
-        return e && *e && *e != '0';
-    }();
+    const bool per_sample = per_sample_forced();
     if (!per_sample && block64_path_applies(layout, compute, updater, check_conv, storage, max_ld))
         return launch_block64_chains(L, kp, storage, gradient, updater, min_ld, max_ld, lds_spread,
                                      stream, kernel_variant);

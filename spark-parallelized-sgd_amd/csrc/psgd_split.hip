@@ -32,7 +32,8 @@
 // add (v = fma(g, 1 - beta, beta v), accum = fma(g, g, accum), w = fma(-lr', u, w), round 4: one
 // rounding fewer each), and the dot is reassociated (per-wave partials, wave trees, the fixed
 // order above) -- all inside the fp64 mode's 1e-9 relative bar. Logistic's multiplier is on every
-// sample's critical path: fp64 takes chain_block64's short-chain 1/(1 + exp(m)) (within ~2 ulp),
+// sample's critical path: fp64 takes the shared recip_one_plus_exp (psgd_device.h: a degree-11 exp core, truncation < 1e-14,
+// v_rcp_f64 + one Newton step; DESIGN.md §4 lists every fp64 divergence),
 // fp32 the hardware exp2 / reciprocal (as chain_block); the row losses (log1pExp) are summed
 // after the chain from the stored margins, off the sequential path.
 #include "psgd_device.h"

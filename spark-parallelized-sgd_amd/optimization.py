@@ -473,6 +473,10 @@ class DriverCheckpoint:
                 state = self._read(fingerprint)
             except IllegalArgumentException as e:
                 err = str(e)
+            except Exception as e:   # unreadable file (truncated zip, old format, I/O error):
+                # forwarded, so every rank raises after the broadcast instead of ranks >= 1
+                # waiting in it for the process-group timeout
+                err = f"checkpoint {self.path}: unreadable ({e!r})"
         if world > 1:
             import torch.distributed as dist
             box = [(state, err, np.asarray(fingerprint).tobytes())]

@@ -63,3 +63,89 @@ def test_block64_break_label():
     assert bench.kernel_name(440).endswith("per sample, per-sample isConverged break)")
     assert bench.kernel_name(461).startswith("chain_sparse64") and bench.kernel_name(461).endswith("break)")
     assert bench.kernel_name(401).endswith("per sample)") and bench.kernel_name(420).endswith("per sample)")
+
+
+def _fake_record(spec, variant=302):
+    """A secondary record shaped as run_workload returns it (after main()'s renames)."""
+    wl = spec.split(":")[0]
+    return {"spec": spec, "samples_per_s": 1.234567e9, "ms_per_step": 3.1234567, "dtype": "f64",
+            "loss": 1.2345e7,
+            "config": {"workload": f"{wl}: " + bench.WORKLOADS[wl][6] + " [this run: 20,000,000 rows]",
+                       "rows_per_gpu": 20_000_000, "d": 4_194_304, "chains_per_gpu": 1024},
+            "roofline": {"bound": "hbm", "achieved": 6543.21, "peak": 8000.0, "unit": "GB/s",
+                         "frac": 0.81790123, "traffic": 2.1e11, "traffic_source": "profiles/r04_c5_f64_pmc.json",
+                         "kernel": bench.kernel_name(variant), "bytes_per_launch": 4.8e10,
+                         "bytes_per_sample": 2416, "avg_kernel_ms": 94.7169, "avg_epoch_ms": 100.36,
+                         "variant": variant, "timing": "HIP events recorded around each chain-kernel launch"},
+            "prewarm": {"seconds": 0.5, "epochs": 4}}
+
+
+def _headline(n_gpus=1):
+    rec = _fake_record("c2")
+    out = {"metric": "training samples/sec (whole node) + achieved HBM GB/s, logistic SGD 1/2/4/8 GPUs",
+           "value": 3.3e9 * n_gpus, "unit": "samples/s", "n_gpus": n_gpus, "steps": 20, "warmup": 5,
+           "ms_per_step": 3.1, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "f32", "data": "synthetic (device-generated, resident in HBM)",
+           "config": rec["config"], "roofline": rec["roofline"], "prewarm": rec["prewarm"]}
+    if n_gpus == 1:
+        cb = {"value": 1.2e7, "unit": "samples/s", "cores": 16, "kind": "port", "host_cpus": 16,
+              "nproc": 256, "sample": "oracle/psgd_oracle.c (fp64 CPU restatement of ParallelizedSGD.scala:"
+                                      "243-270 incl. per-sample isConverged; least_squares, simple), 256 "
+                                      "partitions x 1024 rows, d=512, 40 epochs, 16 threads, 12.0 s"}
+        out["cpu_baseline"] = cb
+        out["cpu_baseline_c1"] = dict(cb, sample="oracle/psgd_oracle.c, the whole c1 epoch (100000 x 100 "
+                                                 "fp64, 4 partitions, 4 threads = local[4]), 30 epochs, 4.0 s")
+    return out
+
+
+def test_final_line_fits_the_driver_tail(tmp_path, capsys):
+    """the 21.7 KB line with 14 full secondaries was not parsed. With the default
+    secondaries the printed line is one JSON object under LINE_LIMIT (< 8 KB) that still carries
+    the headline, roofline, both cpu baselines and every secondary's summary."""
+    import json
+    specs = bench.DEFAULT_SECONDARY.split(",")
+    assert len(specs) == 14
+    records = [_fake_record(s, 420) for s in specs[:-1]] + [{"spec": specs[-1], "error": "RuntimeError: " + "x" * 900}]
+    out = _headline()
+    out["secondary_detail"] = bench.write_detail(str(tmp_path / "detail.json"), out, records)
+    line = bench.final_line(out, records)
+    assert len(line.encode()) < bench.LINE_LIMIT <= 8192
+    assert "\n" not in line
+    got = json.loads(line)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "dtype", "config",
+              "roofline", "cpu_baseline", "cpu_baseline_c1", "secondary_summary"):
+        assert k in got, k
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in got["roofline"], k
+    assert [e["spec"] for e in got["secondary_summary"]] == specs
+    assert all("frac" in e for e in got["secondary_summary"][:-1])
+    assert "secondary" not in got
+    # the full records are in the detail file
+    detail = json.load(open(tmp_path / "detail.json"))
+    assert len(detail["secondary"]) == 14 and detail["secondary"][0]["roofline"]["kernel"]
+
+
+def test_final_line_multi_gpu():
+    import json
+    line = bench.final_line(_headline(8), [])
+    assert len(line) < bench.LINE_LIMIT
+    got = json.loads(line)
+    assert got["n_gpus"] == 8 and "secondary_summary" not in got
+
+
+def test_final_line_shrinks_when_too_long():
+    """A line over the limit drops its descriptive strings, never the numbers."""
+    import json
+    specs = [f"c5:f64:adam:f64" for _ in range(60)]
+    line = bench.final_line(_headline(), [_fake_record(s) for s in specs])
+    assert len(line) < bench.LINE_LIMIT
+    got = json.loads(line)
+    assert len(got["secondary_summary"]) == 60
+    assert "frac" in got["roofline"] and "value" in got
+
+
+def test_bench_prints_its_line_last(monkeypatch, capsys, tmp_path):
+    """main()'s rank-0 output on stdout is exactly one line (the secondaries do not print)."""
+    import inspect
+    src = inspect.getsource(bench.main)
+    assert src.count("print(") == 1 and "final_line(" in src

@@ -50,7 +50,8 @@ def test_kernel_selection_limits_on_the_host(pkg):
     """The dispatch predicates are host code (no device needed). chain_sparse_lds (fp32 and fp64)
     counts a chain's rows in 32 bits, so a partition of more than INT32_MAX rows must not select
     it (such partitions fit in HBM as 16-byte CSR rows); chain_sparse64 takes fp64 CSR
-    with Simple, or SquaredL2 while alpha stays in range, and never the per-sample break."""
+    with Simple, or SquaredL2 while alpha stays in range, with or without the per-sample break
+    (variants 420/421, 460/461)."""
     lib = ctypes.CDLL(pkg._native.LIB_PATH)
     lds = lib._ZN4psgd18sparse_lds_appliesElll
     lds.restype, lds.argtypes = ctypes.c_bool, [ctypes.c_int64] * 3

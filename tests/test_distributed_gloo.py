@@ -216,3 +216,24 @@ def test_two_ranks_checkpoint_rank0_broadcast(tmp_path):
     for r in range(world):
         msg = str(np.load(f"{bad}.rank{r}.err.npz")["msg"])
         assert "other parameters or data than rank 0" in msg, msg
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("kind", ["truncated", "old_format"])
+def test_two_ranks_unreadable_checkpoint_raises_on_every_rank(tmp_path, kind):
+    """an unreadable checkpoint on rank 0 (a truncated zip, an .npz without the
+    version key) is forwarded through the broadcast, so both ranks raise the same error instead
+    of rank 1 waiting in the broadcast for the process-group timeout."""
+    world = 2
+    ck = tmp_path / "ck.npz"
+    if kind == "truncated":
+        np.savez(ck, weights=np.zeros(5), i=np.int64(2))
+        ck.write_bytes(ck.read_bytes()[:40])
+    else:
+        np.savez(ck, weights=np.zeros(5), i=np.int64(2))   # no version / fingerprint keys
+    res = str(tmp_path / "res.npz")
+    mp.start_processes(_ckpt_worker, args=(world, _free_port(), str(ck), 3, res), nprocs=world,
+                       start_method="spawn")
+    for r in range(world):
+        msg = str(np.load(f"{res}.rank{r}.err.npz")["msg"])
+        assert "unreadable" in msg and "ck.npz" in msg, msg

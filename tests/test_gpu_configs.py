@@ -7,7 +7,8 @@
   chain_sparse_spec (variant 411, its 94 KB LDS tag table at this d), and fp64
   through chain_sparse_lds in fp64 (variant 620: an LDS head of ~5k doubles, the tail in HBM).
 * C5 (L2 Logistic CSR, d = 2^22, 100 nnz/row, lambda 1e-6, step 0.5): fp32 chain_sparse
-  (variant 401, HBM-resident weights) and fp64 chain_general's alpha-scaled lazy SquaredL2.
+  (variant 401, HBM-resident weights) and fp64 chain_sparse64 (variant 420: double vectors in HBM,
+  alpha-scaled SquaredL2).
 * psgd_fold_partials_device (the cross-GPU level of the treeReduce, PSGD.scala:271-276) bit for
   bit against the combiner restated in numpy, incl. a zero-count and a NaN-count rank.
 * The engine's two-level fold over partition subsets (what two ranks do) against the oracle's
@@ -170,7 +171,7 @@ def c5():
 
 @pytest.mark.parametrize("compute,want", [("f32", 401), ("f64", 420)])
 def test_c5_wide_sparse_l2(pkg, oracle, c5, compute, want):
-    # f32: chain_sparse (HBM-resident weights); f64: chain_general's alpha-scaled lazy SquaredL2
+    # f32: chain_sparse (HBM-resident weights); f64: chain_sparse64 (double vectors in HBM, alpha-scaled SquaredL2)
     d, rp, col, val, y, offs, w0 = c5
     vs = val.astype(np.float32) if compute == "f32" else val
     data = csr_parts(pkg, y, rp, col, vs, d, offs)

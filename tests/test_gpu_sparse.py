@@ -18,6 +18,7 @@ import numpy as np
 import pytest
 
 from conftest import has_gpu
+from test_gpu_parity import fp32_break_counts_agree
 
 pytestmark = pytest.mark.gpu
 
@@ -351,13 +352,10 @@ def test_sparse_lds_per_sample_break_fp32(pkg, oracle, monkeypatch, grad, upd, h
                                               0.05, 1.0, np.zeros(d), tol, compute_dtype="f32",
                                               return_chain_counts=True)
         assert pkg.optimization.get_context(0).last_kernel() == 641
-        wr, hr, cr = oracle.run(mat, offs, grad, upd, 1.0, 3, 0.05, np.zeros(d), tol=tol, n_threads=8)
+        wr, hr, cr, mg = oracle.run_with_margins(mat, offs, grad, upd, 1.0, 3, 0.05, np.zeros(d), tol=tol,
+                                                 n_threads=8)
         tag = f"fp32 {grad} {upd} head={head} tol={tol}"
-        got = [c for it in counts for c in it]
-        ref = [c for it in cr[: len(counts)] for c in it]
-        same = sum(int(a == b) for a, b in zip(got, ref))
-        assert len(got) == len(ref) and same >= 0.9 * len(ref), (tag, same, len(ref))
-        if same == len(ref) and len(h) == len(hr):
+        if fp32_break_counts_agree(counts, cr, mg, tag) and len(h) == len(hr):
             scale = max(np.max(np.abs(wr)), 1e-30)
             assert np.max(np.abs(w - wr)) / scale <= FP32_REL, tag
             assert np.max(np.abs(h - hr) / np.maximum(np.abs(hr), 1e-30)) <= FP32_LOSS_REL, tag

@@ -134,7 +134,8 @@ def test_golden_fixtures_reproduce(oracle, golden):
                               col=np.array(case["col"]), val=np.array(case["val"]), d=case["d"])
         w, h, c = oracle.run(m, case["offsets"], case["gradient"], case["updater"], case["step"],
                              case["iters"], case["reg"], np.array(case["w0"]), tol=case["tol"],
-                             fraction=case.get("fraction", 1.0), num_classes=case.get("num_classes", 2))
+                             fraction=case.get("fraction", 1.0), num_classes=case.get("num_classes", 2),
+                             margin_check=False)
         e = case["expected"]
         assert list(map(float, w)) == e["weights"], case["name"]
         assert list(map(float, h)) == e["loss_history"], case["name"]
@@ -203,3 +204,30 @@ def test_multinomial_gradient_is_softmax_cross_entropy():
         wp, hp, _ = R.run([([list(X[0])], [lab])], R.GRAD_LOGISTIC, R.UPD_SIMPLE, 1.0, 1, 0.0, list(w0),
                           tol=0.0, num_classes=4)
         assert list(map(float, w)) == wp and list(map(float, h)) == hp
+
+
+def test_break_margin_probe(oracle):
+    """The break-margin probe leaves every decision unchanged and reports, per
+    iteration and chain, the closest |diff / (tol max(norm, 1)) - 1|; the tol-free ratio trace puts
+    a break exactly where tol = r_k (1 +- 1e-13) says: at sample k just above r_k, past it just
+    below (the adversarial cases of tests/test_gpu_break_margin.py)."""
+    rng = np.random.default_rng(5)
+    n, d, P = 400, 12, 4
+    X = rng.standard_normal((n, d)) / np.sqrt(d)
+    y = (X @ rng.standard_normal(d) + rng.logistic(size=n) > 0).astype(float)
+    m = oracle.Matrix(y, X)
+    offs = [i * n // P for i in range(P)] + [n]
+    w, h, c = oracle.run(m, offs, "logistic", "simple", 0.5, 3, 0.0, np.zeros(d), tol=0.02, margin_check=False)
+    w2, h2, c2, mg = oracle.run_with_margins(m, offs, "logistic", "simple", 0.5, 3, 0.0, np.zeros(d), tol=0.02)
+    assert np.array_equal(w, w2) and np.array_equal(h, h2) and np.array_equal(c, c2)
+    assert mg.shape == c.shape and np.all(mg > 0) and np.all(np.isfinite(mg))
+    r = oracle.ratio_trace(m, offs, 1, "logistic", "simple", 0.5, 0.0, np.zeros(d))
+    assert len(r) == offs[2] - offs[1]
+    # a record low of the trace (every earlier sample's r larger by far more than 1e-13)
+    k = next(k for k in range(5, len(r)) if r[k] < r[:k].min() * (1 - 1e-9))
+    for e, want_at_k in ((1e-13, True), (-1e-13, False)):
+        tol = r[k] * (1 + e)
+        _, _, cc = oracle.run(m, offs, "logistic", "simple", 0.5, 1, 0.0, np.zeros(d), tol=tol, margin_check=False)
+        assert (cc[0][1] == k + 1) == want_at_k, (e, cc[0][1], k)
+        _, _, _, mm = oracle.run_with_margins(m, offs, "logistic", "simple", 0.5, 1, 0.0, np.zeros(d), tol=tol)
+        assert mm[0][1] < 2e-13

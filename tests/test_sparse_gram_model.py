@@ -1,4 +1,4 @@
-"""CPU model of chain_sparse_gram's algorithm (tools/experimental/psgd_sparse_gram.hip: a measured
+"""CPU model of chain_sparse_gram's algorithm (tools/experimental/psgd_sparse_gram.hip at commit 3c55d48, since removed from the tree: a measured
 negative result kept out of libpsgd.so), checked against the
 sequential chain of ParallelizedSGD.scala:243-270 in f64.
 
