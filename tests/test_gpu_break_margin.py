@@ -55,13 +55,13 @@ def synth_csr(rng, n, d, kmin, kmax):
 # name: (layout, d, row dtype, compute, updater, reg, step, env, expected variant or None)
 CASES = {
     "block64_h1_simple": ("dense", 60, np.float64, "f64", "simple", 0.0, 4.0 / 60, {}, 741),
-    "block64_h2_simple": ("dense", 700, np.float32, "f64", "simple", 0.0, 4.0 / 700, {}, 752),
-    "block64_h2_l2": ("dense", 700, np.float32, "f64", "squared_l2", 0.05, 4.0 / 700, {}, 752),
+    "block64_h2_simple": ("dense", 700, np.float32, "f64", "simple", 0.0, 4.0 / 700, {}, 754),
+    "block64_h2_l2": ("dense", 700, np.float32, "f64", "squared_l2", 0.05, 4.0 / 700, {}, 754),
     "split_adagrad": ("dense", 700, np.float32, "f64", "adagrad", 0.0, 0.2, {}, None),
     "split_adam": ("dense", 700, np.float32, "f64", "adam", 0.0, 0.2, {}, None),
     "split_l1": ("dense", 700, np.float32, "f64", "l1", 0.002, 0.2, {}, None),
     "split_simple": ("dense", 700, np.float32, "f64", "simple", 0.0, 4.0 / 700, {"PSGD_B64_CONV": "0"}, None),
-    "general_dense": ("dense", 100, np.float64, "f64", "simple", 0.0, 0.04, {"PSGD_PER_SAMPLE": "1"}, None),
+    "per_sample_dense": ("dense", 100, np.float64, "f64", "simple", 0.0, 0.04, {"PSGD_PER_SAMPLE": "1"}, None),
     "sparse_lds64": ("csr", 3000, np.float32, "f64", "simple", 0.0, 1.0, {}, None),
     "sparse_lds64_l2": ("csr", 3000, np.float32, "f64", "squared_l2", 0.05, 1.0, {}, None),
     "sparse64": ("csr", 3000, np.float32, "f64", "simple", 0.0, 1.0, {"PSGD_SPARSE_KERNEL": "hbm64"}, None),
