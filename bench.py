@@ -46,7 +46,7 @@ SECONDARY_ROWS = {"c5": 20_000_000}
 # reference's own Double rows (8,200 B per sample)
 # (AdaGrad / Adam on the logistic c3 shard: the reference's Adam, r^iter in fix1 (UPD.scala:262),
 # turns NaN once the squared-gradient average r exceeds 1, which least squares at c2 reaches)
-DEFAULT_SECONDARY = ("c3:f64::f64,c3:f64,c3:f32,c2:f64,c1:f64,c4:f32,c4:f64,c4:f64::f64,c5:f32,c5:f64,"
+DEFAULT_SECONDARY = ("c3:f32,c3:f64::f64,c3:f64,c2:f64,c1:f64,c4:f32,c4:f64,c4:f64::f64,c5:f32,c5:f64,"
                      "c3:f32:adagrad,c3:f32:adam,c3:f64:adagrad,c3:f64:adam")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
@@ -516,6 +516,8 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
                      "timing": "HIP events recorded around each chain-kernel launch on its stream"},
         "prewarm": {"seconds": prewarm_s, "epochs": prewarm_epochs},   # untimed, model discarded
         "_meta": (grad, d, P, step, csr, upd_name, reg),
+        # per timed step, the chain kernel's ms (the detail file only; the stdout line drops it)
+        "kernel_ms_series": [round(x, 4) for x in kernel_ms],
     }
     del engine, data, parts, all_parts
     return res
@@ -563,6 +565,7 @@ def main():
                        args.chains, args.updater, args.storage, args.backend, args.skew_rows, args.tol)
     grad, d, P, step, csr, upd_name, reg = res.pop("_meta")
     res.pop("loss")
+    series = res.pop("kernel_ms_series")
     out = {
         "metric": "training samples/sec (whole node) + achieved HBM GB/s, logistic SGD 1/2/4/8 GPUs",
         "value": res["value"], "unit": "samples/s", "n_gpus": world, "steps": args.steps,
@@ -598,8 +601,8 @@ def main():
         r["loss"] = float(r["loss"])
         records.append(r)
     if rank == 0:
-        if records:
-            out["secondary_detail"] = write_detail(args.detail, out, records)
+        if records or args.detail:
+            out["detail_file"] = write_detail(args.detail, dict(out, kernel_ms_series=series), records)
         print(final_line(out, records), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -638,7 +641,7 @@ def final_line(out, records):
     """The ONE stdout JSON line: headline fields, roofline, cpu baselines and the compact
     secondary summary. Never longer than LINE_LIMIT bytes: if it would be, the roofline's and
     the cpu baselines' descriptive strings are dropped first, then the summary's extra fields."""
-    line = dict(out)
+    line = {k: v for k, v in out.items() if k != "kernel_ms_series"}
     if records:
         line["secondary_summary"] = secondary_summary(records)
     s = json.dumps(line, separators=(",", ":"))

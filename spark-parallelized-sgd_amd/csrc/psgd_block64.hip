@@ -21,13 +21,16 @@
 // row i's update needs ||w_i - w_{i+1}|| and ||w_{i+1}||, and both follow from scalars the block
 // already has. With w' = a w + c x (a = 1 for Simple), z = x . w (the row's dot) and q = x . x
 // (the Gram diagonal, which the Gram waves add to their slot):
-//     ||w'||^2       = a (a ||w||^2 + 2 c z) + c^2 q
-//     ||w - w'||^2   = b (b ||w||^2 - 2 c z) + c^2 q,   b = 1 - a
+//     ||w'||^2       = a^2 ||w||^2 + c (2 a z + c q)
+//     ||w - w'||^2   = b^2 ||w||^2 + c (c q - 2 b z),   b = s lambda (= 1 - a)
 // and the test sqrt(D) < tol max(sqrt(N), 1) is D < tol^2 max(N, 1). ||w||^2 starts exact (the
-// chain waves' partial norms of w_in) and follows the recurrence, in the chain's sample order;
-// only a ratio within ~1e-12 of tol could decide differently from the oracle's sums over the
-// rounded vectors. The first row that passes ends the chain: the rows after it in the block take
-// c = 0, a = 1 (no update, loss or count) and no later block runs.
+// chain waves' partial norms of w_in) and follows these affine maps in the chain's sample order:
+// round 5 evaluates a block's 8 tests at once after its recurrence (a segmented scan over the
+// rows' maps, block64's CONV section), not row by row on the recurrence's dependent path. Every
+// fp64 kernel decides as the oracle down to tol = r (1 +- 1e-13) (tests/test_gpu_break_margin.py).
+// The first row that passes ends the chain: the updates of the block's later rows, issued
+// interleaved with the recurrence, are undone (W restored from the block start, the taken rows
+// replayed: once per chain), their loss and count dropped, and no later block runs.
 //
 // Why blocks in fp64: the per-sample kernel (chain_dense) has the dot's wave reduction, an f64
 // exp and a division and the update on one dependent path per sample (~400 ns at d = 100). Here
@@ -116,6 +119,17 @@ __device__ __forceinline__ double reduce32d(const double (&v)[32], int lane) {
 // Lane that carries row i of a block after reduce8d (one with k(l) = i and l&7 = 0).
 __host__ __device__ constexpr int row_lane64(int i) {
     return 32 * (i & 1) + 16 * ((i >> 1) & 1) + 8 * ((i >> 2) & 1);
+}
+
+// Lane `addr / 4`'s value (ds_bpermute on both halves).
+__device__ __forceinline__ double bperm_d(double v, int addr) {
+    const int lo = __builtin_amdgcn_ds_bpermute(addr, (int)lo32(v));
+    const int hi = __builtin_amdgcn_ds_bpermute(addr, (int)hi32(v));
+    return mk64((unsigned)lo, (unsigned)hi);
+}
+// The value of the lane `sh` below inside a row of 16 (DPP row_shr; 0 past the row's start).
+__device__ __forceinline__ double dpp_shr(double v, int sh) {
+    return sh == 1 ? dpp_mov<0x111>(v) : sh == 2 ? dpp_mov<0x112>(v) : dpp_mov<0x114>(v);
 }
 
 #ifndef PSGD_B64_FAST_SIGMOID
@@ -627,35 +641,24 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
         };
         bool brk = false;   // CONV: a row of this block passed isConverged
         int keff = kk;      // the rows taken
+        // CONV: this lane's row's coefficient (lane row_lane64(k) computes c_k at step k), and W
+        // at the block start (the updates run interleaved with the recurrence, before the block's
+        // break test; a break -- once per chain -- restores W and replays the rows it takes)
+        double ck = 0.0;
+        double wsave[(CONV && PSGD_B64_INTERLEAVE) ? EH : 1];
+        if constexpr (CONV && PSGD_B64_INTERLEAVE) {
+#pragma unroll
+            for (int e = 0; e < EH; ++e) wsave[e] = w[e];
+        }
 #pragma unroll
         for (int i = 0; i < kB; ++i) {
-            c[i] = readlane_d(coef64<GRAD>(z, yv, nsv), row_lane64(i));
+            const double cv = coef64<GRAD>(z, yv, nsv);
+            c[i] = readlane_d(cv, row_lane64(i));
             if constexpr (TAIL) c[i] = i < kk ? c[i] : 0.0;
-            if constexpr (CONV) c[i] = brk ? 0.0 : c[i];   // rows after the break are not taken
+            if constexpr (CONV) ck = krow == i ? cv : ck;
             if constexpr (UPD == U_SQUARED_L2) {
                 al[i] = readlane_d(alpha, row_lane64(i));
                 if constexpr (TAIL) al[i] = i < kk ? al[i] : 1.0;
-                if constexpr (CONV) al[i] = brk ? 1.0 : al[i];
-            }
-            if constexpr (CONV) {
-                // isConverged(w_i, w_{i+1}) (PSGD.scala:262, :333-335) from the recurrences in the
-                // header: z_i (lane row_lane64(i)'s dot, before this step moves it), q_i, c_i, a_i
-                const double zi = readlane_d(z, row_lane64(i));
-                const double qi = readlane_d(q, row_lane64(i));
-                const double cq = c[i] * c[i] * qi;
-                double nn, dd;
-                if constexpr (UPD == U_SQUARED_L2) {
-                    const double ai = al[i], bi = 1.0 - ai;
-                    nn = ai * __builtin_fma(ai, nsq, 2.0 * c[i] * zi) + cq;
-                    dd = bi * __builtin_fma(bi, nsq, -2.0 * c[i] * zi) + cq;
-                } else {
-                    nn = __builtin_fma(c[i], 2.0 * zi, nsq) + cq;
-                    dd = cq;
-                }
-                nsq = nn > 0.0 ? nn : 0.0;
-                const bool pass = (!TAIL || i < kk) && !brk && dd < tol2 * (nn > 1.0 ? nn : 1.0);
-                keff = pass ? i + 1 : keff;
-                brk = brk || pass;
             }
             if constexpr (UPD == U_SQUARED_L2) {
                 if (krow == i) zf = z;
@@ -668,6 +671,74 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
             if constexpr (PSGD_B64_INTERLEAVE) update_row(i);
         }
         if constexpr (UPD != U_SQUARED_L2) zf = z;
+        if constexpr (CONV) {
+            // isConverged(w_k, w_{k+1}) (PSGD.scala:262, :333-335) for the block's rows at once:
+            // with w' = a w + c x, z = x . w (zf: the row's dot before its step) and q = x . x,
+            // ||w_{k+1}||^2 = a^2 ||w_k||^2 + c (2 a z + c q) is an affine map of ||w_k||^2 per row
+            // and D_k = ||w_k - w_{k+1}||^2 = b^2 N_k + c (c q - 2 b z) with b = s lambda. The
+            // rows' terms move to lanes 8m + k (ds_bpermute), a segmented scan over each 8-lane
+            // group (DPP row_shr 1, 2, 4) gives N_k and N_{k+1} from the block start's norm, and the
+            // first row with D_k < tol^2 max(N_{k+1}, 1) ends the chain. (Round 4 ran the test per
+            // row, ~10 dependent f64 operations on the chain waves: c2 fp64 +51 % over tol 0.)
+            const bool live = !TAIL || krow < kk;
+            const double c_ = live ? ck : 0.0;
+            const double cq1 = c_ * q;
+            const int kl = lane & 7;                        // the row this lane carries below
+            const int src = row_lane64(kl) * 4;             // a lane of row kl (bpermute address)
+            double Nn, dd;
+            if constexpr (UPD == U_SQUARED_L2) {
+                const double a_ = live ? alpha : 1.0, b_ = sv * lam;
+                double A = bperm_d(a_ * a_, src);
+                double B = bperm_d(c_ * __builtin_fma(2.0 * a_, zf, cq1), src);
+                const double b2 = bperm_d(b_ * b_, src);
+                const double E = bperm_d(c_ * __builtin_fma(-2.0 * b_, zf, cq1), src);
+#pragma unroll
+                for (int sh = 1; sh < kB; sh *= 2) {   // (this after the earlier one)
+                    const double oA = dpp_shr(A, sh), oB = dpp_shr(B, sh);
+                    const bool take = kl >= sh;
+                    const double nB = __builtin_fma(A, oB, B);
+                    A = take ? A * oA : A;
+                    B = take ? nB : B;
+                }
+                Nn = __builtin_fma(A, nsq, B);
+                double Nk = dpp_shr(Nn, 1);
+                Nk = kl == 0 ? nsq : Nk;
+                dd = __builtin_fma(b2, Nk, E);
+            } else {
+                double B = bperm_d(c_ * __builtin_fma(2.0, zf, cq1), src);
+                dd = bperm_d(c_ * cq1, src);
+#pragma unroll
+                for (int sh = 1; sh < kB; sh *= 2) {
+                    const double oB = dpp_shr(B, sh);
+                    B = kl >= sh ? oB + B : B;
+                }
+                Nn = nsq + B;
+            }
+            // lanes 0 .. 7 decide rows 0 .. 7 (rows >= kk carry no step and never pass)
+            const bool pass = lane < kB && (!TAIL || kl < kk) && dd < tol2 * (Nn > 1.0 ? Nn : 1.0);
+            const unsigned long long m = __builtin_amdgcn_ballot_w64(pass);
+            if constexpr (PSGD_B64_INTERLEAVE) {
+                // the interleaved updates stay ahead of the test (the compiler would otherwise
+                // sink them into the no-break branch, off the recurrence they are there to fill)
+#pragma unroll
+                for (int e = 0; e < EH; ++e) asm volatile("" : "+v"(w[e]));
+            }
+            if (m != 0ull) {   // a row passed: the first one ends the chain (once per chain)
+                const int kstar = __builtin_ctzll(m);
+                brk = true;
+                keff = kstar + 1;
+                if constexpr (PSGD_B64_INTERLEAVE) {
+#pragma unroll
+                    for (int e = 0; e < EH; ++e) w[e] = wsave[e];
+#pragma unroll
+                    for (int i = 0; i < kB; ++i)
+                        if (i <= kstar) update_row(i);
+                }
+            } else {
+                const double nb = readlane_d(Nn, kB - 1);   // rows >= kk are identities
+                nsq = nb > 0.0 ? nb : 0.0;
+            }
+        }
         if (lead) {
             if constexpr (LOSS_EXT) {
                 if (loss_lane && ((!TAIL && !CONV) || krow < keff)) zout[t0 + krow] = zf;
@@ -684,7 +755,8 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
         // W <- a_i W + c_i x_i, i = 0..kB-1, in sample order
         if constexpr (!PSGD_B64_INTERLEAVE) {
 #pragma unroll
-            for (int i = 0; i < kB; ++i) update_row(i);
+            for (int i = 0; i < kB; ++i)
+                if (i < keff) update_row(i);
         }
         PSGD_STAMP(st_upd += __builtin_amdgcn_s_memtime() - st_c;)
         rs += kB;

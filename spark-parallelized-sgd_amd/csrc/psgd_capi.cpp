@@ -114,15 +114,32 @@ inline int64_t xorshift_hash_seed(int64_t s) {
 }
 }  // namespace sampling
 
+// Physically contiguous device memory (hipDeviceMallocContiguous) for the buffers the chains
+// access at random: the CSR kernels' per-chain weight vectors (c5: 17 / 34 GB of scattered
+// gathers and stores). Falls back to hipMalloc when no contiguous range is free.
+// PSGD_CONTIG=0 turns it off (A/B measurements; read at every allocation).
+static bool contig_enabled() {
+    const char* e = getenv("PSGD_CONTIG");
+    return !(e && e[0] == '0');
+}
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
-    hipError_t ensure(size_t need) {
+    hipError_t ensure(size_t need, bool contiguous = false) {
         if (need <= bytes) return hipSuccess;
         if (p) hipFree(p);
         p = nullptr;
         bytes = 0;
-        hipError_t e = hipMalloc(&p, need);
+        hipError_t e = hipErrorOutOfMemory;
+        if (contiguous && contig_enabled()) {
+            e = hipExtMallocWithFlags(&p, need, hipDeviceMallocContiguous);
+            if (e != hipSuccess) {
+                (void)hipGetLastError();
+                p = nullptr;
+            }
+        }
+        if (e != hipSuccess) e = hipMalloc(&p, need);
         if (e == hipSuccess) bytes = need;
         return e;
     }
@@ -987,7 +1004,7 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         // 128 + 1024 floats the kernels' masked-off lanes load from / store to)
         // (rows 256-byte aligned: the epoch's init kernel stores 16-byte vectors)
         L.wstride = ((int64_t)d + 128 + 1024 + 63) / 64 * 64;
-        HIP_TRY(ctx->wf32.ensure((size_t)P * (size_t)L.wstride * sizeof(float)));
+        HIP_TRY(ctx->wf32.ensure((size_t)P * (size_t)L.wstride * sizeof(float), true));
         HIP_TRY(ctx->walpha.ensure((size_t)P * sizeof(double)));
         HIP_TRY(ctx->wnsq0.ensure(sizeof(double)));
         L.wf32 = ctx->wf32.as<float>();
@@ -1005,7 +1022,7 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         // kernels will run (chain_general keeps its weights in w_out, and C5's
         // vectors are ~34 GB); if HBM cannot hold them the epoch runs chain_general instead.
         const int64_t stride = 2 * (((int64_t)d + 128 + 1024 + 63) / 64 * 64);
-        if (ctx->wf32.ensure((size_t)P * (size_t)stride * sizeof(float)) == hipSuccess) {
+        if (ctx->wf32.ensure((size_t)P * (size_t)stride * sizeof(float), true) == hipSuccess) {
             HIP_TRY(ctx->walpha.ensure((size_t)P * sizeof(double)));
             HIP_TRY(ctx->wnsq0.ensure(sizeof(double)));
             L.wstride = stride;

@@ -107,7 +107,7 @@ def test_final_line_fits_the_driver_tail(tmp_path, capsys):
     assert len(specs) == 14
     records = [_fake_record(s, 420) for s in specs[:-1]] + [{"spec": specs[-1], "error": "RuntimeError: " + "x" * 900}]
     out = _headline()
-    out["secondary_detail"] = bench.write_detail(str(tmp_path / "detail.json"), out, records)
+    out["detail_file"] = bench.write_detail(str(tmp_path / "detail.json"), out, records)
     line = bench.final_line(out, records)
     assert len(line.encode()) < bench.LINE_LIMIT <= 8192
     assert "\n" not in line

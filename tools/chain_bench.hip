@@ -33,9 +33,9 @@ static int launch(const psgd::ChainLaunch& L, const psgd::KParams& kp, int grad,
     const size_t lds = 160 * 1024 - 512;
 #define NVCASE(G, U)                                                                              \
     if (grad == G && upd == U) {                                                                  \
-        if (d == 256) return psgd::launch_block<float, G, U, 1>(L, kp, true, lds, 0);             \
-        if (d == 512) return psgd::launch_block<float, G, U, 2>(L, kp, true, lds, 0);             \
-        if (d == 1024) return psgd::launch_block<float, G, U, 4>(L, kp, true, lds, 0);            \
+        if (d == 256) return psgd::launch_block<float, G, U, 1, false>(L, kp, true, lds, 0);             \
+        if (d == 512) return psgd::launch_block<float, G, U, 2, false>(L, kp, true, lds, 0);             \
+        if (d == 1024) return psgd::launch_block<float, G, U, 4, false>(L, kp, true, lds, 0);            \
     }
     NVCASE(0, 0) NVCASE(1, 0) NVCASE(0, 1) NVCASE(1, 1)
 #undef NVCASE

@@ -6,7 +6,7 @@
 //   loader:       total, blocked on a full ring, in its vmcnt wait
 //   Gram waves:   total, waiting for rows
 // Usage: chain_bench64 <rows per chain> <chains> <d> <grad 0|1|2> <upd 0|1> [storage bytes 4|8]
-//                      [chain waves 1|2]
+//                      [chain waves 1|2] [tol: > 0 runs the per-sample break instance]
 #define PSGD_STAMPS 1
 #define PSGD_NO_DISPATCH 1
 #include "../spark-parallelized-sgd_amd/csrc/psgd_block64.hip"
@@ -39,24 +39,28 @@ __global__ void fill_d(double* x, size_t n, double v) {
 
 // f64 compute on f32 rows (d = 256 / 512 / 1024: NV = 1 / 2 / 4) or f64 rows (d = 512 / 1024:
 // NV = 4 / 8), full rows; H chain waves
-template <typename S, int H>
+template <typename S, int H, bool C>
 static int launch_s(const psgd::ChainLaunch& L, const psgd::KParams& kp, int grad, int upd, int d) {
     const size_t lds = 160 * 1024 - 512;
     constexpr int VEC = 16 / sizeof(S);
 #define NVCASE(G, U)                                                                              \
     if (grad == G && upd == U) {                                                                  \
-        if constexpr (H == 1) if (d == 64 * VEC) return psgd::launch_block64<S, G, U, 1, 1>(L, kp, true, lds, 0); \
-        if (d == 128 * VEC) return psgd::launch_block64<S, G, U, 2, H>(L, kp, true, lds, 0);      \
-        if (d == 256 * VEC) return psgd::launch_block64<S, G, U, 4, H>(L, kp, true, lds, 0);      \
-        if constexpr (H == 2) if (d == 512 * VEC) return psgd::launch_block64<S, G, U, 8, 2>(L, kp, true, lds, 0); \
+        if constexpr (H == 1) if (d == 64 * VEC) return psgd::launch_block64<S, G, U, 1, 1, C>(L, kp, true, lds, 0); \
+        if (d == 128 * VEC) return psgd::launch_block64<S, G, U, 2, H, C>(L, kp, true, lds, 0);      \
+        if (d == 256 * VEC) return psgd::launch_block64<S, G, U, 4, H, C>(L, kp, true, lds, 0);      \
+        if constexpr (H == 2) if (d == 512 * VEC) return psgd::launch_block64<S, G, U, 8, 2, C>(L, kp, true, lds, 0); \
     }
     NVCASE(0, 0) NVCASE(1, 0) NVCASE(0, 1) NVCASE(1, 1)
 #undef NVCASE
     return -3;
 }
+template <bool C>
+static int launch_c(const psgd::ChainLaunch& L, const psgd::KParams& kp, int grad, int upd, int d, int es, int H) {
+    if (es == 4) return H == 1 ? launch_s<float, 1, C>(L, kp, grad, upd, d) : launch_s<float, 2, C>(L, kp, grad, upd, d);
+    return H == 1 ? launch_s<double, 1, C>(L, kp, grad, upd, d) : launch_s<double, 2, C>(L, kp, grad, upd, d);
+}
 static int launch(const psgd::ChainLaunch& L, const psgd::KParams& kp, int grad, int upd, int d, int es, int H) {
-    if (es == 4) return H == 1 ? launch_s<float, 1>(L, kp, grad, upd, d) : launch_s<float, 2>(L, kp, grad, upd, d);
-    return H == 1 ? launch_s<double, 1>(L, kp, grad, upd, d) : launch_s<double, 2>(L, kp, grad, upd, d);
+    return kp.tol > 0.0 ? launch_c<true>(L, kp, grad, upd, d, es, H) : launch_c<false>(L, kp, grad, upd, d, es, H);
 }
 
 int main(int argc, char** argv) {
@@ -67,6 +71,7 @@ int main(int argc, char** argv) {
     const int upd = argc > 5 ? atoi(argv[5]) : 0;
     const int es = argc > 6 ? atoi(argv[6]) : 4;
     const int H = argc > 7 ? atoi(argv[7]) : 2;
+    const double tol = argc > 8 ? atof(argv[8]) : 0.0;   // > 0: the per-sample break instance
     const size_t nx = (size_t)rows * P * d;
     float* X; double* Xd = nullptr; double *y, *steps, *w_in, *w_out, *rv, *loss, *cnt_d; int64_t* cnt; int* wd;
     unsigned long long* stamps;
@@ -104,7 +109,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&zbuf, (size_t)rows * P * 8));
     L.zbuf64 = zbuf; L.zstride = rows;
     psgd::KParams kp{};
-    kp.reg = 0.01; kp.d = d; kp.n_chains = P;
+    kp.reg = 0.01; kp.d = d; kp.n_chains = P; kp.tol = tol;
     hipEvent_t a, b;
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
     int variant = 0;

@@ -5,7 +5,7 @@
 //   plain1   : 1 wave per workgroup, global_load_dwordx4, 8 rows in flight
 //   ldsdma   : ring_loader (the chain kernels' loader) + a consumer wave that hands every slot
 //              straight back (no compute): the loader/handshake ceiling
-// Usage: stream_bench <rows per partition> <partitions> <R ring rows> <D depth>
+// Usage: stream_bench <rows per partition> <partitions> <R ring rows> <D depth> [nv]
 #include "../spark-parallelized-sgd_amd/csrc/psgd_device.h"
 
 #include <hip/hip_runtime.h>
@@ -83,6 +83,28 @@ __global__ __launch_bounds__(NW * 64) void dmaraw(const float4* __restrict__ X, 
     int slot = 0;
     for (int64_t i = a; i < b; ++i) {
         __builtin_amdgcn_global_load_lds((const void*)(as_global(base + i * 64 + lane)),
+                                         (__attribute__((address_space(3))) void*)(region + slot * 1024), 16, 0, 0);
+        slot = (slot + 1) & 31;
+        wait_vmcnt_le(D);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// dmaraw with the partitions' rows interleaved in HBM: groups of G rows (nv 1 KiB pieces each)
+// round-robin over the P partitions, so at any moment the CUs read neighbouring addresses.
+template <int NW, int D>
+__global__ __launch_bounds__(NW * 64) void dmaint(const float4* __restrict__ X, int64_t rows_per, int nv, int G) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t P = gridDim.x, gp = (int64_t)G * nv;   // pieces per group
+    // whole groups only: piece index ((i / gp) P + p) gp + i % gp stays below P * total
+    const int64_t total = rows_per * nv / gp * gp;
+    const int64_t a = total * wave / NW, b = total * (wave + 1) / NW;
+    char* region = smem + wave * 32768;
+    int slot = 0;
+    for (int64_t i = a; i < b; ++i) {
+        const int64_t piece = ((i / gp) * P + blockIdx.x) * gp + i % gp;
+        __builtin_amdgcn_global_load_lds((const void*)(as_global(X + piece * 64 + lane)),
                                          (__attribute__((address_space(3))) void*)(region + slot * 1024), 16, 0, 0);
         slot = (slot + 1) & 31;
         wait_vmcnt_le(D);
@@ -190,11 +212,29 @@ int main(int argc, char** argv) {
     const int P = argc > 2 ? atoi(argv[2]) : 256;
     const int R = argc > 3 ? atoi(argv[3]) : 64;
     const int D = argc > 4 ? atoi(argv[4]) : 28;
-    const int nv = 2;  // d = 512 f32
+    const int nv = argc > 5 ? atoi(argv[5]) : 2;  // 1 KiB vectors per row: 2 = d 512 f32 (c2), 4 = c3
     const int64_t rowbytes = nv * 1024;
     const size_t bytes = (size_t)rows * P * rowbytes;
+    // [6] GB allocated, written and freed before the stream's buffer (a process that ran another
+    // workload first); [7] 1: the stream's buffer from hipExtMallocWithFlags(hipDeviceMallocContiguous)
+    const double pre_gb = argc > 6 ? atof(argv[6]) : 0.0;
+    const int contig = argc > 7 ? atoi(argv[7]) : 0;
+    if (pre_gb > 0) {
+        void* T;
+        const size_t tb = (size_t)(pre_gb * 1e9);
+        CK(hipMalloc(&T, tb));
+        CK(hipMemset(T, 1, tb));
+        CK(hipDeviceSynchronize());
+        CK(hipFree(T));
+    }
     void* X;
-    CK(hipMalloc(&X, bytes));
+    if (contig) {
+        hipError_t e = hipExtMallocWithFlags(&X, bytes, hipDeviceMallocContiguous);
+        printf("contiguous allocation of %.1f GB: %s\n", bytes / 1e9, hipGetErrorString(e));
+        if (e != hipSuccess) { (void)hipGetLastError(); CK(hipMalloc(&X, bytes)); }
+    } else {
+        CK(hipMalloc(&X, bytes));
+    }
     CK(hipMemset(X, 0, bytes));
     double* y; double* steps; int* wd; float* out;
     CK(hipMalloc(&y, rows * P * 8)); CK(hipMemset(y, 0, rows * P * 8));
@@ -237,7 +277,21 @@ int main(int argc, char** argv) {
     RS(1, 32) RS(2, 16) RS(4, 8) RS(4, 16) RS(8, 8) RS(8, 16) RS(16, 4) RS(16, 8)
 #define DR(NW, D) CK(hipFuncSetAttribute((const void*)dmaraw<NW, D>, hipFuncAttributeMaxDynamicSharedMemorySize, NW * 32768)); \
     timeit("dma" #NW "x" #D, [&] { hipLaunchKernelGGL((dmaraw<NW, D>), dim3(P), dim3(NW * 64), NW * 32768, 0, (const float4*)X, rows, nv); });
-    DR(1, 16) DR(1, 32) DR(1, 56) DR(2, 16) DR(2, 28) DR(4, 8) DR(4, 14)
+    DR(1, 16) DR(1, 32) DR(1, 56) DR(2, 16) DR(2, 28) DR(2, 56) DR(4, 8) DR(4, 14) DR(4, 28)
+    // host check of the interleaved kernel's largest piece index (whole groups of G rows only)
+    for (int G : {1, 8, 64, 512}) {
+        const int64_t gp = (int64_t)G * nv, tot = rows * nv / gp * gp;
+        const int64_t maxp = (((tot - 1) / gp) * P + (P - 1)) * gp + (tot - 1) % gp;
+        if (tot <= 0 || maxp >= (int64_t)rows * nv * P) { fprintf(stderr, "dmaint bounds G=%d\n", G); return 1; }
+    }
+#define DI(NW, D, G) CK(hipFuncSetAttribute((const void*)dmaint<NW, D>, hipFuncAttributeMaxDynamicSharedMemorySize, NW * 32768)); \
+    timeit("int" #NW "x" #D "g" #G, [&] { hipLaunchKernelGGL((dmaint<NW, D>), dim3(P), dim3(NW * 64), NW * 32768, 0, (const float4*)X, rows, nv, G); });
+    DI(1, 56, 8) DI(2, 28, 8) DI(4, 14, 8) DI(2, 28, 1) DI(2, 28, 64) DI(2, 28, 512)
+    DR(2, 28) DR(4, 14)
+    if (nv != 2) return 0;   // the ring-loader variants below are NV = 2 instances
+    // (and they need a ring deeper than their depth plus two groups: a shallower ring with the
+    // consumed check can wait forever -- R = 32 with D = 28 hung, r05)
+    if (R < D + 16) return 0;
     const int MB = (R + kMetaRows - 1) / kMetaRows + 2;
     RingGeom g{R, MB, D, 0};
     const size_t lds = sizeof(RingHeader) + (size_t)MB * kMetaBlockBytes + (size_t)R * rowbytes;
