@@ -175,6 +175,8 @@ def parse():
     ap.add_argument("--tol", type=float, default=0.0,
                     help="convergenceTol of the headline workload (PSGD.scala:262 per-sample break; the "
                          "reference's default is 0.001; BASELINE's configs run 0)")
+    ap.add_argument("--no-arena", action="store_true",
+                    help="allocate each workload's rows separately (A/B of the one-allocation arena)")
     ap.add_argument("--detail", default=os.path.join("gpurun_out", "bench_detail.json"),
                     help="file for the full secondary records ('' = none); stdout carries a summary")
     ap.add_argument("--prewarm-s", type=float, default=1.0,
@@ -182,17 +184,57 @@ def parse():
     return ap.parse_args()
 
 
-def make_shard(torch, dev, n, d, P, grad, dtype, seed, skew=0):
+class Arena:
+    """One device allocation, made at the start of the process, that every workload's synthetic
+    rows are carved from (the partitions of a persisted RDD are registered once and stay resident;
+    the bench does not allocate and free 20-100 GB per workload). Measured round 5: a dense
+    workload whose rows were allocated after another workload's 51-102 GB had been freed streamed
+    5-7 % slower (profiles/r05_c3_stream_ceiling.log item 4); carved from one arena every workload
+    runs on the process's first allocation."""
+
+    def __init__(self, torch, dev, nbytes):
+        self.buf = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=dev)
+        self.off = 0
+
+    def take(self, shape, dtype):
+        import math
+        n = math.prod(shape) * dtype.itemsize
+        if self.off + n > self.buf.numel():
+            raise MemoryError(f"arena: {n} bytes past its {self.buf.numel()}")
+        t = self.buf[self.off:self.off + n].view(dtype).view(shape)
+        self.off += (n + 4095) // 4096 * 4096
+        return t
+
+    def reset(self):
+        self.off = 0
+
+
+def shard_bytes(workload, storage="", rows=0, features=0, skew=0, chains=0):
+    """Bytes of a workload's synthetic rows and labels in the arena (4 KiB rounding per tensor)."""
+    grad, n, d, P, step, sdt = WORKLOADS[workload][:6]
+    sdt = storage or sdt
+    n = rows or n
+    d = features or d
+    P = chains or P
+    es = 4 if sdt == "f32" else 8
+    pad = 3 * 4096
+    if workload in CSR_NNZ:
+        nnz = CSR_NNZ[workload]
+        return n * nnz * (4 + es) + n * 8 + pad
+    return (n + P * skew) * d * es + n * 8 + pad
+
+
+def make_shard(torch, dev, n, d, P, grad, dtype, seed, skew=0, arena=None):
     """Synthetic rows in HBM: X ~ N(0,1); w* ~ N(0, 1/d); LeastSquares y = w*.x + N(0, 0.01);
     Logistic y = 1{w*.x + Logistic(0,1) > 0}. skew > 0: partition p's rows start
-    p * skew rows later in the allocation (unused rows in between)."""
+    p * skew rows later in the allocation (unused rows in between). X and y from `arena` if given."""
     g = torch.Generator(device=dev)
     g.manual_seed(seed)
     tdt = torch.float32 if dtype == "f32" else torch.float64
-    X = torch.empty((n + P * skew, d), dtype=tdt, device=dev)
+    X = arena.take((n + P * skew, d), tdt) if arena else torch.empty((n + P * skew, d), dtype=tdt, device=dev)
     chunk = 1 << 20
     w_star = torch.randn(d, generator=g, device=dev, dtype=torch.float64) / d ** 0.5
-    y = torch.empty(n, dtype=torch.float64, device=dev)
+    y = arena.take((n,), torch.float64) if arena else torch.empty(n, dtype=torch.float64, device=dev)
     for a in range(0, n, chunk):
         b = min(n, a + chunk)
         X[a:b].normal_(generator=g)
@@ -211,7 +253,7 @@ def make_shard(torch, dev, n, d, P, grad, dtype, seed, skew=0):
     return X, y, offs
 
 
-def make_csr_shard(torch, dev, n, d, P, grad, dtype, seed, nnz):
+def make_csr_shard(torch, dev, n, d, P, grad, dtype, seed, nnz, arena=None):
     """Synthetic rcv1-like CSR rows in HBM: nnz distinct sorted indices per
     row (one uniform draw in each of nnz equal column buckets), values U(0,1) L2-normalised per
     row, labels y = 1{w*.x + Logistic(0,1) > 0} from a planted w* ~ N(0,1)."""
@@ -219,9 +261,12 @@ def make_csr_shard(torch, dev, n, d, P, grad, dtype, seed, nnz):
     g.manual_seed(seed)
     tdt = torch.float32 if dtype == "f32" else torch.float64
     width = d // nnz
-    col = torch.empty((n, nnz), dtype=torch.int32, device=dev)
-    val = torch.empty((n, nnz), dtype=tdt, device=dev)
-    y = torch.empty(n, dtype=torch.float64, device=dev)
+    if arena:
+        col, val, y = arena.take((n, nnz), torch.int32), arena.take((n, nnz), tdt), arena.take((n,), torch.float64)
+    else:
+        col = torch.empty((n, nnz), dtype=torch.int32, device=dev)
+        val = torch.empty((n, nnz), dtype=tdt, device=dev)
+        y = torch.empty(n, dtype=torch.float64, device=dev)
     w_star = torch.randn(d, generator=g, device=dev, dtype=torch.float64)
     base = (torch.arange(nnz, device=dev, dtype=torch.int64) * width)[None, :]
     chunk = 1 << 18
@@ -337,7 +382,7 @@ def cpu_baseline_c1(budget_s, seed=42):
 
 def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, rows, fraction,
                  steps, warmup, prewarm_s, features=0, chains=0, updater="", storage="", backend="nccl",
-                 skew=0, tol=0.0):
+                 skew=0, tol=0.0, arena=None):
     """One workload: synthetic shard in HBM, prewarm, W warmup steps, K timed steps (barrier +
     synchronize on both sides, max over ranks). Returns the measurement as a dict."""
     import numpy as np
@@ -361,12 +406,12 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
     csr = workload in CSR_NNZ
     if csr:
         rp, col, val, y, offs = make_csr_shard(torch, dev, n, d, P, grad, sdt, 1000 + rank,
-                                               CSR_NNZ[workload])
+                                               CSR_NNZ[workload], arena)
         torch.cuda.synchronize()
         parts = [pkg.DeviceCsrPartition(y[a:b], rp[a:b + 1], col, val, d) for a, b in zip(offs[:-1], offs[1:])]
         empty = lambda: pkg.DeviceCsrPartition(y[:0], rp[:1], col, val, d)
     else:
-        X, y, offs = make_shard(torch, dev, n, d, P, grad, sdt, 1000 + rank, skew)
+        X, y, offs = make_shard(torch, dev, n, d, P, grad, sdt, 1000 + rank, skew, arena)
         torch.cuda.synchronize()
         parts = [pkg.DevicePartition(y[a:b], X[a + p * skew:b + p * skew], d)
                  for p, (a, b) in enumerate(zip(offs[:-1], offs[1:]))]
@@ -560,9 +605,18 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
+    secondary = [s for s in args.secondary.split(",") if s] if world == 1 else []
+    arena = None
+    if not args.no_arena:
+        need = shard_bytes(args.workload, args.storage, args.rows, args.features, args.skew_rows, args.chains)
+        for spec in secondary:
+            wl, _, _, sto = (spec.split(":") + ["", "", ""])[:4]
+            need = max(need, shard_bytes(wl, sto, SECONDARY_ROWS.get(wl, 0)))
+        arena = Arena(torch, dev, need)
     res = run_workload(torch, dist, pkg, dev, rank, world, local, args.workload, args.compute,
                        args.rows, args.fraction, args.steps, args.warmup, args.prewarm_s, args.features,
-                       args.chains, args.updater, args.storage, args.backend, args.skew_rows, args.tol)
+                       args.chains, args.updater, args.storage, args.backend, args.skew_rows, args.tol,
+                       arena=arena)
     grad, d, P, step, csr, upd_name, reg = res.pop("_meta")
     res.pop("loss")
     series = res.pop("kernel_ms_series")
@@ -583,15 +637,16 @@ def main():
         out["cpu_baseline_c1"] = cpu_baseline_c1(min(args.cpu_seconds, 4.0))
     # Secondary lines (one GPU only): the other BASELINE configs' per-GPU workloads under the
     # same clock, each with its own roofline (VERDICT r01 "let the driver observe" them).
-    secondary = [s for s in args.secondary.split(",") if s] if world == 1 else []
     records = []
     for spec in secondary:
         wl, comp, upd, sto = (spec.split(":") + ["", "", ""])[:4]
         torch.cuda.empty_cache()
+        if arena:
+            arena.reset()   # the previous workload's rows are dead: the next one reuses the memory
         try:
             r = run_workload(torch, dist, pkg, dev, rank, world, local, wl, comp or "f32",
                              SECONDARY_ROWS.get(wl, 0), 1.0, args.steps, args.warmup,
-                             min(args.prewarm_s, 0.5), updater=upd, storage=sto)
+                             min(args.prewarm_s, 0.5), updater=upd, storage=sto, arena=arena)
         except Exception as e:   # a secondary line never hides the headline
             records.append({"spec": spec, "error": f"{type(e).__name__}: {e}"})
             continue

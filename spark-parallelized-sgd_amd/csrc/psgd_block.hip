@@ -111,6 +111,18 @@ __device__ __forceinline__ float readlane_f(float v, int lane) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
 
+// Lane `addr / 4`'s double (ds_bpermute on both halves); a double of the lane `sh` below in a row
+// of 16 (DPP row_shr, 0 past the row's start).
+__device__ __forceinline__ double bperm_d32(double v, int addr) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const int lo = __builtin_amdgcn_ds_bpermute(addr, (int)(unsigned)b);
+    const int hi = __builtin_amdgcn_ds_bpermute(addr, (int)(unsigned)(b >> 32));
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ double dpp_shr_d(double v, int sh) {
+    return sh == 1 ? dpp_mov<0x111>(v) : sh == 2 ? dpp_mov<0x112>(v) : dpp_mov<0x114>(v);
+}
+
 // c = -s * mult(z, y) for the gradient (vector form; only lane row_lane(i) matters at step i).
 //   Logistic: mult = 1/(1+exp(-z)) - y;  LeastSquares: mult = z - y;  Hinge: mult = 1 > ls*z ? -ls : 0
 template <int GRAD>
@@ -356,7 +368,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     int rs = 0, gs = 0, ms = 0;      // ring slot, Gram slot and meta block of the current block
     const int64_t nfull = n / kBlk;
     const int ntail = (int)(n - nfull * kBlk);
-    const float tol2 = float(kp.tol * kp.tol);
     bool conv_stop = false;   // CONV: a row passed isConverged, the chain has ended
     PSGD_STAMP(const uint64_t st_begin = __builtin_amdgcn_s_memtime(); uint64_t st_rd = 0, st_gr = 0, st_p = 0, st_rec = 0, st_upd = 0;)
 
@@ -475,35 +486,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         float zf = z;
         bool brk = false;   // CONV: a row of this block passed isConverged
         int keff = kk;      // the rows taken
+        float ck = 0.0f;    // CONV: this lane's row's coefficient (lane row_lane(k) computes c_k at step k)
 #pragma unroll
         for (int i = 0; i < kBlk; ++i) {
-            c[i] = readlane_f(coef<GRAD>(z, yv, sv, nsv, aux), row_lane(i));
+            const float cv = coef<GRAD>(z, yv, sv, nsv, aux);
+            c[i] = readlane_f(cv, row_lane(i));
             if constexpr (TAIL) c[i] = i < kk ? c[i] : 0.0f;
-            if constexpr (CONV) c[i] = brk ? 0.0f : c[i];   // rows after the break are not taken
+            if constexpr (CONV) ck = krow == i ? cv : ck;
             if constexpr (UPD == U_SQUARED_L2) {
                 al[i] = readlane_f(alpha, row_lane(i));
                 if constexpr (TAIL) al[i] = i < kk ? al[i] : 1.0f;
-                if constexpr (CONV) al[i] = brk ? 1.0f : al[i];
-            }
-            if constexpr (CONV) {
-                // isConverged(w_i, w_{i+1}) from z_i (Logistic: the recurrence carries u), q_i, c_i
-                float zi = readlane_f(z, row_lane(i));
-                if constexpr (GRAD == G_LOGISTIC) zi *= kLn2Neg;
-                const float qi = readlane_f(q, row_lane(i));
-                const float cq = c[i] * c[i] * qi;
-                float nn, dd;
-                if constexpr (UPD == U_SQUARED_L2) {
-                    const float ai = al[i], bi = 1.0f - ai;
-                    nn = ai * __builtin_fmaf(ai, nsq, 2.0f * c[i] * zi) + cq;
-                    dd = bi * __builtin_fmaf(bi, nsq, -2.0f * c[i] * zi) + cq;
-                } else {
-                    nn = __builtin_fmaf(c[i], 2.0f * zi, nsq) + cq;
-                    dd = cq;
-                }
-                nsq = nn > 0.0f ? nn : 0.0f;
-                const bool pass = (!TAIL || i < kk) && !brk && dd < tol2 * (nn > 1.0f ? nn : 1.0f);
-                keff = pass ? i + 1 : keff;
-                brk = brk || pass;
             }
             if constexpr (UPD == U_SQUARED_L2) {
                 if (krow == i) zf = z;
@@ -513,6 +505,109 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             }
         }
         if constexpr (UPD != U_SQUARED_L2) zf = z;
+        // W <- a_i W + c_i x_i for the block's rows in sample order (CONV: every row, as if no
+        // row passes; W at the block start is kept for the rare block where one does)
+        auto update_rows = [&](int last) __attribute__((always_inline)) {
+#pragma unroll
+            for (int i = 0; i < kBlk; ++i) {
+                if (i > last) break;
+                const T2 ci = T2{c[i], c[i]};
+                if constexpr (KEEP) {
+#pragma unroll
+                    for (int e = 0; e < E2; ++e) {
+                        if constexpr (UPD == U_SQUARED_L2)
+                            w[e] = __builtin_elementwise_fma(ci, xr[i][e], w[e] * T2{al[i], al[i]});
+                        else
+                            w[e] = __builtin_elementwise_fma(ci, xr[i][e], w[e]);
+                    }
+                } else if (!TAIL || i < kk) {
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) {
+                        T2 xv[H];
+                        to_pairs(read_vec(base + i * ROW_BYTES, v), xv);
+#pragma unroll
+                        for (int h = 0; h < H; ++h) {
+                            const int e = v * H + h;
+                            if constexpr (UPD == U_SQUARED_L2)
+                                w[e] = __builtin_elementwise_fma(ci, xv[h], w[e] * T2{al[i], al[i]});
+                            else
+                                w[e] = __builtin_elementwise_fma(ci, xv[h], w[e]);
+                        }
+                    }
+                }
+            }
+        };
+        if constexpr (CONV) {
+            // isConverged(w_k, w_{k+1}) (PSGD.scala:262, :324-336) for the block's rows at once, in
+            // f64 (as the CSR kernels' conv_step): with w' = a w + c x, z = x . w and
+            // q = x . x, ||w_{k+1}||^2 = a^2 ||w_k||^2 + c (2 a z + c q) and
+            // ||w_k - w_{k+1}||^2 = b^2 ||w_k||^2 + c (c q - 2 b z) with b = s lambda taken directly
+            // (1 - a is 0 in fp32 once s lambda < 2^-25). The rows' terms move to lanes 8m + k
+            // (ds_bpermute) and a segmented DPP scan from the block start's exact ||W||^2 gives
+            // every row's norms; the first row with D_k < tol^2 max(N_{k+1}, 1) ends the chain.
+            // The block's updates run between the bpermutes and the scan (their latency), as if no
+            // row passed; on a pass (once per chain) W is restored and the taken rows replayed.
+            const bool live = !TAIL || krow < kk;
+            const double c_ = live ? double(ck) : 0.0;
+            double zd = double(zf);
+            if constexpr (GRAD == G_LOGISTIC) zd *= double(kLn2Neg);   // u -> the dot
+            const double cq1 = c_ * double(q);
+            const int kl = lane & 7;
+            const int src = row_lane(kl) * 4;
+            const double n0 = double(nsq);
+            double A = 1.0, B, b2 = 0.0, E;
+            if constexpr (UPD == U_SQUARED_L2) {
+                const double a_ = live ? double(alpha) : 1.0, b_ = meta.y * kp.reg;
+                A = bperm_d32(a_ * a_, src);
+                B = bperm_d32(c_ * __builtin_fma(2.0 * a_, zd, cq1), src);
+                b2 = bperm_d32(b_ * b_, src);
+                E = bperm_d32(c_ * __builtin_fma(-2.0 * b_, zd, cq1), src);
+            } else {
+                B = bperm_d32(c_ * __builtin_fma(2.0, zd, cq1), src);
+                E = bperm_d32(c_ * cq1, src);
+            }
+            T2 wsave[E2];
+#pragma unroll
+            for (int e = 0; e < E2; ++e) wsave[e] = w[e];
+            update_rows(kBlk - 1);
+            double Nn, dd;
+            if constexpr (UPD == U_SQUARED_L2) {
+#pragma unroll
+                for (int sh = 1; sh < kBlk; sh *= 2) {   // (this after the earlier one)
+                    const double oA = dpp_shr_d(A, sh), oB = dpp_shr_d(B, sh);
+                    const bool take = kl >= sh;
+                    const double nB = __builtin_fma(A, oB, B);
+                    A = take ? A * oA : A;
+                    B = take ? nB : B;
+                }
+                Nn = __builtin_fma(A, n0, B);
+                double Nk = dpp_shr_d(Nn, 1);
+                Nk = kl == 0 ? n0 : Nk;
+                dd = __builtin_fma(b2, Nk, E);
+            } else {
+#pragma unroll
+                for (int sh = 1; sh < kBlk; sh *= 2) {
+                    const double oB = dpp_shr_d(B, sh);
+                    B = kl >= sh ? oB + B : B;
+                }
+                Nn = n0 + B;
+                dd = E;
+            }
+            const double tol2d = kp.tol * kp.tol;
+            const bool pass = (lane < kBlk) & (!TAIL || kl < kk) & (dd < tol2d * (Nn > 1.0 ? Nn : 1.0));   // branch-free
+            // the updates stay ahead of the test (not sunk into its no-pass branch)
+#pragma unroll
+            for (int e = 0; e < E2; ++e) asm volatile("" : "+v"(w[e]));
+            const unsigned long long m = __builtin_amdgcn_ballot_w64(pass);
+            if (m != 0ull) {   // the first passing row ends the chain (once per chain)
+                const int kstar = __builtin_ctzll(m);
+                brk = true;
+                keff = kstar + 1;
+#pragma unroll
+                for (int e = 0; e < E2; ++e) w[e] = wsave[e];
+                update_rows(kstar);
+            }
+        }
         PSGD_STAMP(const uint64_t st_c = __builtin_amdgcn_s_memtime(); st_rec += st_c - st_b;)
         if constexpr (LOSS_EXT) {
             if (loss_lane && ((!TAIL && !CONV) || krow < keff)) zout[t0 + krow] = zf * kLn2Neg;   // u -> dot
@@ -524,35 +619,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         count += keff;
         if constexpr (CONV) conv_stop = brk;
         if (rpre > ready) ready = rpre;   // the next block's wait_rows rarely reads the flag again
-
-        // W <- a_i W + c_i x_i, i = 0..kk-1, in sample order
-#pragma unroll
-        for (int i = 0; i < kBlk; ++i) {
-            const T2 ci = T2{c[i], c[i]};
-            if constexpr (KEEP) {
-#pragma unroll
-                for (int e = 0; e < E2; ++e) {
-                    if constexpr (UPD == U_SQUARED_L2)
-                        w[e] = __builtin_elementwise_fma(ci, xr[i][e], w[e] * T2{al[i], al[i]});
-                    else
-                        w[e] = __builtin_elementwise_fma(ci, xr[i][e], w[e]);
-                }
-            } else if (!TAIL || i < kk) {
-#pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    T2 xv[H];
-                    to_pairs(read_vec(base + i * ROW_BYTES, v), xv);
-#pragma unroll
-                    for (int h = 0; h < H; ++h) {
-                        const int e = v * H + h;
-                        if constexpr (UPD == U_SQUARED_L2)
-                            w[e] = __builtin_elementwise_fma(ci, xv[h], w[e] * T2{al[i], al[i]});
-                        else
-                            w[e] = __builtin_elementwise_fma(ci, xv[h], w[e]);
-                    }
-                }
-            }
-        }
+        if constexpr (!CONV) update_rows(kBlk - 1);
         if constexpr (!KEEP) {
             __hip_atomic_store(&hdr->consumed, (unsigned)(t0 + kk), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);

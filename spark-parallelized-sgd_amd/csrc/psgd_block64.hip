@@ -242,6 +242,19 @@ static_assert(kFixed64 % 16 == 0, "the meta and row rings start 16-byte aligned"
 template <bool CONV>
 constexpr int gram_slot64() { return kB * kB + (CONV ? kB : 0); }
 
+// The Gram work split by features (round 5): from PSGD_B64_FSPLIT_NV row vectors on (c3 with the
+// reference's f64 rows: NV = 8, 2 blocks of 8 KiB rows in the LDS ring), both Gram waves take every
+// block, each over half of the row's vectors, into a sub-slot of their own; the chain waves add the
+// halves. A Gram wave's half of a block fits its registers, so it reads it first and hands the
+// ring slots back before the pair dots (the undivided Gram read one vector of every row at a time
+// and held the slots for its whole ~2,300 cycles: at c3 f64 rows the chain waited ~300 cycles per
+// row for it, the loader was blocked on the full ring half the time; tools/chain_bench64 stamps).
+#ifndef PSGD_B64_FSPLIT_NV
+#define PSGD_B64_FSPLIT_NV 8
+#endif
+template <int NV>
+constexpr bool gram_fsplit64() { return PSGD_B64_FSPLIT_NV > 0 && NV >= PSGD_B64_FSPLIT_NV && NV >= 2; }
+
 template <typename S, int GRAD, int UPD, int NV, bool FULL, int H, bool CONV>
 __global__ __launch_bounds__(64 * (3 + H)) __attribute__((amdgpu_waves_per_eu(H, H)))
 void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
@@ -258,6 +271,8 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
     // wave roles (role_of_waves): chain waves 0 .. H-1, Gram waves 2 and 3, the loader
     constexpr int kRoleLoader = H == 1 ? 1 : 4;
     constexpr int GSZ = gram_slot64<CONV>();
+    constexpr bool FS = gram_fsplit64<NV>();
+    constexpr int GSL = FS ? 2 * GSZ : GSZ;   // doubles per block in the Gram ring
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // LDS: [RingHeader 16 B][GramHeader64 16 B][XchgHeader64 32 B][exchange 36 doubles]
     //      [meta ring MB x 256 B][Gram ring GS x GSZ doubles][row ring R x ROW_BYTES]
@@ -268,7 +283,7 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
     char* meta_ring = smem + kFixed64;
     double* gring = reinterpret_cast<double*>(meta_ring + geom.meta_blocks * kMetaBlockBytes);
     const int GS = geom.gslots;
-    char* ring = reinterpret_cast<char*>(gring + GS * GSZ);
+    char* ring = reinterpret_cast<char*>(gring + GS * GSL);
 
     const int lane = threadIdx.x & 63;
     const int chain = blockIdx.x;
@@ -296,7 +311,7 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
         xhdr->start[1] = 0;
     }
     // entries on and above the diagonal stay zero (the Gram waves write only i < k)
-    for (int i = threadIdx.x; i < GS * GSZ; i += blockDim.x) gring[i] = 0.0;
+    for (int i = threadIdx.x; i < GS * GSL; i += blockDim.x) gring[i] = 0.0;
     // every wave's SIMD, for the role assignment (the exchange area is free until the chain starts)
     unsigned* simd_of = reinterpret_cast<unsigned*>(xchg);
     if (lane == 0) simd_of[threadIdx.x >> 6] = wave_simd();
@@ -305,7 +320,7 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
     __syncthreads();   // the SIMD table is read by every wave before the exchange area is used
 
     if (wave == kRoleLoader) {
-        ring_loader<S, NV, FULL, kB, kB, H>(L, dsc, hdr, meta_ring, ring, geom, lane, ghdr->gread);
+        ring_loader<S, NV, FULL, kB, kB, H, FS>(L, dsc, hdr, meta_ring, ring, geom, lane, ghdr->gread);
         return;
     }
 
@@ -350,16 +365,20 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
         unsigned ready = 0;
         unsigned done = 0;
         PSGD_STAMP(const uint64_t st_begin = __builtin_amdgcn_s_memtime(); uint64_t st_rd = 0;)
-        int rs = gw * kB;            // ring slot of the block's first row (R is a multiple of 16)
-        int gs = gw;                 // Gram slot of the block
-        for (int64_t b = gw; b < nblk; b += 2) {
+        // FS: every block, vectors [v0, v0 + NVG) of its rows; else alternate blocks, every vector
+        constexpr int BSTEP = FS ? 1 : 2;
+        constexpr int NVG = FS ? NV / 2 : NV;
+        const int v0 = FS ? gw * NVG : 0;
+        int rs = FS ? 0 : gw * kB;   // ring slot of the block's first row (R is a multiple of 16)
+        int gs = FS ? 0 : gw;        // Gram slot of the block
+        for (int64_t b = FS ? 0 : gw; b < nblk; b += BSTEP) {
             const int64_t t0 = b * kB;
             const int64_t kk = (n - t0) < kB ? (n - t0) : kB;
             PSGD_STAMP(const uint64_t st_w = __builtin_amdgcn_s_memtime();)
             if (!wait_ready(ready, t0 + kk, 4)) break;
             PSGD_STAMP(st_rd += __builtin_amdgcn_s_memtime() - st_w;)
             const char* base = ring + rs * ROW_BYTES;
-            rs += 2 * kB;
+            rs += BSTEP * kB;
             if (rs >= R) rs -= R;
             double acc[kPairs];
 #pragma unroll
@@ -367,6 +386,32 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
             double dg[kB];   // CONV: the rows' squared norms (the Gram diagonal)
 #pragma unroll
             for (int k = 0; k < kB; ++k) dg[k] = 0.0;
+            if constexpr (FS) {
+                // this wave's half of the block into registers, the slots back, then the dots
+                double xa[NVG][kB][VEC];
+#pragma unroll
+                for (int v = 0; v < NVG; ++v)
+#pragma unroll
+                    for (int k = 0; k < kB; ++k) read_vec(base + k * ROW_BYTES, v0 + v, xa[v][k]);
+                asm volatile("s_waitcnt lgkmcnt(0)" : : : "memory");
+                __hip_atomic_store(&ghdr->gread[gw], done + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+                for (int v = 0; v < NVG; ++v) {
+                    int q = 0;
+#pragma unroll
+                    for (int k = 1; k < kB; ++k)
+#pragma unroll
+                        for (int i = 0; i < k; ++i, ++q)
+#pragma unroll
+                            for (int hh = 0; hh < VEC; ++hh) acc[q] = __builtin_fma(xa[v][k][hh], xa[v][i][hh], acc[q]);
+                    if constexpr (CONV) {
+#pragma unroll
+                        for (int k = 0; k < kB; ++k)
+#pragma unroll
+                            for (int hh = 0; hh < VEC; ++hh) dg[k] = __builtin_fma(xa[v][k][hh], xa[v][k][hh], dg[k]);
+                    }
+                }
+            } else {
             // one 16-byte vector of every row at a time (f64 rows of a whole block would not
             // fit the registers at NV >= 4)
 #pragma unroll
@@ -400,14 +445,15 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
             // every row of the block has been read: hand its ring slots back
             asm volatile("s_waitcnt lgkmcnt(0)" : : : "memory");
             __hip_atomic_store(&ghdr->gread[gw], done + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
             double g[32];
 #pragma unroll
             for (int q = 0; q < kPairs; ++q) g[q] = acc[q];
 #pragma unroll
             for (int q = kPairs; q < 32; ++q) g[q] = 0.0;
             const double val = reduce32d(g, lane);
-            double* slot = gring + gs * GSZ;
-            gs += 2;
+            double* slot = gring + gs * GSL + (FS ? gw * GSZ : 0);
+            gs += BSTEP;
             if (gs >= GS) gs -= GS;
             if (goff >= 0) slot[goff] = val;
             if constexpr (CONV) {
@@ -540,7 +586,11 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
         // block is handed back): free the ring slots (the loader also waits for the Gram)
         __hip_atomic_store(my_consumed, (unsigned)(t0 + kk), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         // flags this block tests, read now so that their LDS round trip lands under the dots
-        const unsigned gpre = __hip_atomic_load(&ghdr->gdone[b & 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        unsigned gpre = __hip_atomic_load(&ghdr->gdone[FS ? 0 : (b & 1)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if constexpr (FS) {
+            const unsigned g1 = __hip_atomic_load(&ghdr->gdone[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            gpre = g1 < gpre ? g1 : gpre;
+        }
         const unsigned rpre = __hip_atomic_load(&hdr->ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         PSGD_STAMP(const uint64_t st_a = __builtin_amdgcn_s_memtime();)
         // p_k = x_k . W over this wave's features
@@ -569,13 +619,21 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
             __hip_atomic_store(&xhdr->xdone[h], (unsigned)(b + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         PSGD_STAMP(const uint64_t st_b = __builtin_amdgcn_s_memtime(); st_p += st_b - st_a;)
-        // the block's Gram triangle (Gram wave b&1 publishes its blocks in order)
+        // the block's Gram triangle (Gram wave b&1 publishes its blocks in order; FS: both halves)
         {
-            const unsigned need = (unsigned)(b >> 1) + 1;
-            unsigned* gd = &ghdr->gdone[b & 1];
+            const unsigned need = FS ? (unsigned)b + 1 : (unsigned)(b >> 1) + 1;
+            unsigned* gd = &ghdr->gdone[FS ? 0 : (b & 1)];
+            auto gdone_now = [&]() __attribute__((always_inline)) -> unsigned {
+                unsigned g = __hip_atomic_load(gd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if constexpr (FS) {
+                    const unsigned g1 = __hip_atomic_load(&ghdr->gdone[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    g = g1 < g ? g1 : g;
+                }
+                return g;
+            };
             if (gpre < need) {
                 const uint64_t tw = __builtin_amdgcn_s_memrealtime();
-                while (__hip_atomic_load(gd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+                while (gdone_now() < need) {
                     if (__builtin_amdgcn_s_memrealtime() - tw > kWatchdogTicks) {
                         __hip_atomic_fetch_or(L.watchdog, 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         __hip_atomic_store(&hdr->stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -585,16 +643,24 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
             }
         }
         PSGD_STAMP(const uint64_t st_g = __builtin_amdgcn_s_memtime(); st_gr += st_g - st_b;)
-        const double* grow = gring + gs * GSZ + krow * kB;
+        const double* grow = gring + gs * GSL + krow * kB;
         double G[kB];
 #pragma unroll
         for (int q = 0; q < kB / 2; ++q) {
             const f64x2 g2 = *reinterpret_cast<const f64x2*>(grow + 2 * q);
             G[2 * q] = g2.x;
             G[2 * q + 1] = g2.y;
+            if constexpr (FS) {   // the second Gram wave's half of the features
+                const f64x2 h2 = *reinterpret_cast<const f64x2*>(grow + GSZ + 2 * q);
+                G[2 * q] += h2.x;
+                G[2 * q + 1] += h2.y;
+            }
         }
         double q = 0.0;   // CONV: the squared norm of this lane's row
-        if constexpr (CONV) q = gring[gs * GSZ + kB * kB + krow];
+        if constexpr (CONV) {
+            q = gring[gs * GSL + kB * kB + krow];
+            if constexpr (FS) q += gring[gs * GSL + GSZ + kB * kB + krow];
+        }
         if constexpr (H == 2) {
             // the other chain wave's partial of this lane's row: z = p0 + p1 in both waves
             const unsigned need = (unsigned)(b + 1);
@@ -715,7 +781,7 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
                 Nn = nsq + B;
             }
             // lanes 0 .. 7 decide rows 0 .. 7 (rows >= kk carry no step and never pass)
-            const bool pass = lane < kB && (!TAIL || kl < kk) && dd < tol2 * (Nn > 1.0 ? Nn : 1.0);
+            const bool pass = (lane < kB) & (!TAIL || kl < kk) & (dd < tol2 * (Nn > 1.0 ? Nn : 1.0));   // branch-free
             const unsigned long long m = __builtin_amdgcn_ballot_w64(pass);
             if constexpr (PSGD_B64_INTERLEAVE) {
                 // the interleaved updates stay ahead of the test (the compiler would otherwise
@@ -847,7 +913,8 @@ static int launch_block64(const ChainLaunch& L, const KParams& kp, bool full, si
     auto bytes_for = [&](int r) {
         const int mb = (r + kMetaRows - 1) / kMetaRows + 2;
         const int gs = r / kB + 1;
-        return kFixed64 + (size_t)mb * kMetaBlockBytes + (size_t)gs * gram_slot64<CONV>() * 8 + (size_t)r * ROW;
+        return kFixed64 + (size_t)mb * kMetaBlockBytes +
+               (size_t)gs * gram_slot64<CONV>() * 8 * (gram_fsplit64<NV>() ? 2 : 1) + (size_t)r * ROW;
     };
     int R = (int)((budget - kFixed64) / ROW) / kB * kB;
     while (R > 0 && bytes_for(R) > budget) R -= kB;

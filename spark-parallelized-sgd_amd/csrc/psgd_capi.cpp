@@ -114,13 +114,14 @@ inline int64_t xorshift_hash_seed(int64_t s) {
 }
 }  // namespace sampling
 
-// Physically contiguous device memory (hipDeviceMallocContiguous) for the buffers the chains
-// access at random: the CSR kernels' per-chain weight vectors (c5: 17 / 34 GB of scattered
-// gathers and stores). Falls back to hipMalloc when no contiguous range is free.
-// PSGD_CONTIG=0 turns it off (A/B measurements; read at every allocation).
+// PSGD_CONTIG=1: physically contiguous device memory (hipDeviceMallocContiguous) for the CSR
+// kernels' per-chain weight vectors (A/B measurements; read at every allocation; falls back to
+// hipMalloc when no contiguous range is free). Off by default: measured round 5, it made c5 fp32
+// 1.4 % faster and steadier (107.2 ms against 108.7) but c4 31 -> 45 ms (fp32) and c5 fp64 95 -> 117 ms
+// (the chains' vectors at a regular physical stride).
 static bool contig_enabled() {
     const char* e = getenv("PSGD_CONTIG");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
 }
 
 struct DevBuf {

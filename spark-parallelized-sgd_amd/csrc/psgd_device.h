@@ -449,9 +449,11 @@ __device__ __forceinline__ void lds_store_u32_nowait(unsigned* p, unsigned v) {
 
 // GB > 0: rows are also read by two helper waves that take alternate blocks of GB rows and
 // count their finished blocks in gdone[0] (even blocks) / gdone[1] (odd blocks); a slot is free
-// only once both the consumer and its helper are done with it. CONS = 2: two consumers, the
-// second counting in hdr->consumed1; a slot is free once both have passed it.
-template <typename S, int NV, bool FULL, int PUB, int GB = 0, int CONS = 1>
+// only once both the consumer and its helper are done with it. GALL: both helpers read every
+// block (each a share of its features) and count in gdone[0] / gdone[1]; a block is free once
+// both have passed it. CONS = 2: two consumers, the second counting in hdr->consumed1; a slot is
+// free once both have passed it.
+template <typename S, int NV, bool FULL, int PUB, int GB = 0, int CONS = 1, bool GALL = false>
 __device__ __forceinline__ void ring_loader(const ChainLaunch& L, const ChainDesc& dsc, RingHeader* hdr,
                                             char* meta_ring, char* ring, const RingGeom& geom,
                                             int lane, const unsigned* gdone = nullptr) {
@@ -517,7 +519,8 @@ __device__ __forceinline__ void ring_loader(const ChainLaunch& L, const ChainDes
                     const unsigned g0 = __builtin_amdgcn_readfirstlane(lds_load_u32_asm(&gdone[0]));
                     const unsigned g1 = __builtin_amdgcn_readfirstlane(lds_load_u32_asm(&gdone[1]));
                     // blocks 0 .. min(2 g0, 2 g1 + 1) - 1 are all done by their helper
-                    const unsigned gb = 2 * g0 < 2 * g1 + 1 ? 2 * g0 : 2 * g1 + 1;
+                    // (GALL: blocks 0 .. min(g0, g1) - 1 by both)
+                    const unsigned gb = GALL ? (g0 < g1 ? g0 : g1) : 2 * g0 < 2 * g1 + 1 ? 2 * g0 : 2 * g1 + 1;
                     c = c < gb * GB ? c : gb * GB;
                 }
                 limit = (int64_t)c + R;

@@ -149,3 +149,28 @@ def test_bench_prints_its_line_last(monkeypatch, capsys, tmp_path):
     import inspect
     src = inspect.getsource(bench.main)
     assert src.count("print(") == 1 and "final_line(" in src
+
+
+def test_arena_carves_aligned_views_and_resets():
+    """The one-allocation arena of the synthetic shards (bench.Arena) hands out non-overlapping,
+    4 KiB-aligned views of one buffer, refuses to overrun it, and is reused after reset()."""
+    import pytest
+    import torch
+    a = bench.Arena(torch, torch.device("cpu"), bench.shard_bytes("c1"))
+    X = a.take((100_000, 100), torch.float64)
+    y = a.take((100_000,), torch.float64)
+    assert X.shape == (100_000, 100) and y.shape == (100_000,)
+    base = a.buf.data_ptr()
+    assert (X.data_ptr() - base) % 4096 == 0 and (y.data_ptr() - base) % 4096 == 0
+    assert y.data_ptr() >= X.data_ptr() + X.numel() * 8
+    X.fill_(1.0)
+    y.fill_(2.0)
+    assert float(X.sum()) == 1e7 and float(y.sum()) == 2e5
+    with pytest.raises(MemoryError):
+        a.take((1 << 20,), torch.float64)
+    a.reset()
+    assert a.take((10,), torch.float32).data_ptr() == X.data_ptr()
+    # every default workload fits the arena sized for it
+    for spec in bench.DEFAULT_SECONDARY.split(","):
+        wl, _, _, sto = (spec.split(":") + ["", "", ""])[:4]
+        assert bench.shard_bytes(wl, sto, bench.SECONDARY_ROWS.get(wl, 0)) < 110e9

@@ -3,7 +3,7 @@
 //   chain wave: total, waiting for rows, waiting for the Gram triangle
 //   loader:     total, blocked on a full ring, in its vmcnt wait
 //   Gram waves: total, waiting for rows
-// Usage: chain_bench <rows per chain> <chains> <d> <grad 0|1|2> <upd 0|1>
+// Usage: chain_bench <rows per chain> <chains> <d> <grad 0|1|2> <upd 0|1> [tol: > 0 = the break instance]
 #define PSGD_STAMPS 1
 #define PSGD_NO_DISPATCH 1
 #include "../spark-parallelized-sgd_amd/csrc/psgd_block.hip"
@@ -29,17 +29,21 @@ __global__ void fill_d(double* x, size_t n, double v) {
 }
 
 // only the f32 instantiations the bench shapes use (d = 256 / 512 / 1024: NV = 1 / 2 / 4, full rows)
-static int launch(const psgd::ChainLaunch& L, const psgd::KParams& kp, int grad, int upd, int d) {
+template <bool C>
+static int launch_c(const psgd::ChainLaunch& L, const psgd::KParams& kp, int grad, int upd, int d) {
     const size_t lds = 160 * 1024 - 512;
 #define NVCASE(G, U)                                                                              \
     if (grad == G && upd == U) {                                                                  \
-        if (d == 256) return psgd::launch_block<float, G, U, 1, false>(L, kp, true, lds, 0);             \
-        if (d == 512) return psgd::launch_block<float, G, U, 2, false>(L, kp, true, lds, 0);             \
-        if (d == 1024) return psgd::launch_block<float, G, U, 4, false>(L, kp, true, lds, 0);            \
+        if (d == 256) return psgd::launch_block<float, G, U, 1, C>(L, kp, true, lds, 0);          \
+        if (d == 512) return psgd::launch_block<float, G, U, 2, C>(L, kp, true, lds, 0);          \
+        if (d == 1024) return psgd::launch_block<float, G, U, 4, C>(L, kp, true, lds, 0);         \
     }
     NVCASE(0, 0) NVCASE(1, 0) NVCASE(0, 1) NVCASE(1, 1)
 #undef NVCASE
     return -3;
+}
+static int launch(const psgd::ChainLaunch& L, const psgd::KParams& kp, int grad, int upd, int d) {
+    return kp.tol > 0.0 ? launch_c<true>(L, kp, grad, upd, d) : launch_c<false>(L, kp, grad, upd, d);
 }
 
 int main(int argc, char** argv) {
@@ -48,6 +52,7 @@ int main(int argc, char** argv) {
     const int d = argc > 3 ? atoi(argv[3]) : 512;
     const int grad = argc > 4 ? atoi(argv[4]) : 1;
     const int upd = argc > 5 ? atoi(argv[5]) : 0;
+    const double tol = argc > 6 ? atof(argv[6]) : 0.0;   // > 0: the per-sample break instance
     const size_t nx = (size_t)rows * P * d;
     float* X; double *y, *steps, *w_in, *w_out, *rv, *loss, *cnt_d; int64_t* cnt; int* wd;
     unsigned long long* stamps;
@@ -78,7 +83,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&zbuf, (size_t)rows * P * 4));
     L.zbuf = zbuf; L.zstride = rows;
     psgd::KParams kp{};
-    kp.reg = 0.01; kp.d = d; kp.n_chains = P;
+    kp.reg = 0.01; kp.d = d; kp.n_chains = P; kp.tol = tol;
     hipEvent_t a, b;
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
     int variant = 0;
