@@ -55,6 +55,10 @@
 namespace psgd {
 
 constexpr int LCAP = 128;                  // entries per row (two per lane)
+#ifndef PSGD_LDS_TB
+#define PSGD_LDS_TB 4                      // rows per tagger step (their LDS round trips overlap;
+                                           // 8 measured round 5: c4 fp32 28.9 -> 43.3 ms, fp64 56.9 -> 58.0)
+#endif
 #ifndef PSGD_LDS_EXP
 #define PSGD_LDS_EXP 0                     // cost probes (tools/r03_c4_probe.sh); 0 in the product
 #endif
@@ -370,7 +374,7 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
         // sweeps, then each row's tag lookups and updates in row order (one wave's LDS operations
         // execute in program order, so row u+1's lookups see row u's updates), then the rows'
         // addresses.
-        constexpr int TB = 4;
+        constexpr int TB = PSGD_LDS_TB;
         unsigned loaded = 0;
         uint16_t* dtag = reinterpret_cast<uint16_t*>(&hdr->dtag);
         const int32_t chunk = ((NT + kSweepRows - 1) / kSweepRows + 255) & ~int32_t(255);
