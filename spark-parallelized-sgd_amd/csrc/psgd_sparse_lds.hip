@@ -392,6 +392,9 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
                 ca[q] = sl.col[lane];
                 cb[q] = sl.col[lane + 64];
             }
+            // the loader's count for the next step's check, read with the columns (a refresh in
+            // wait_for waits for every LDS access in flight, this step's tag writes included)
+            const unsigned ld_pre = __hip_atomic_load(&hdr->loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             // sweep the chunks of rows u0 .. u0 + TB - 1, keeping the tags of rows u0 - SK .. u0 - 1
             // (the oldest rows this step's lookups need); each chunk is swept at least every
             // kSweepRows rows, so no tag outlives 256 rows
@@ -467,6 +470,7 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
                 }
             }
             publish(&hdr->tagged, u0 + nb);
+            loaded = ld_pre > loaded ? ld_pre : loaded;
         }
         stamp_out(2);
         return;
@@ -568,6 +572,11 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
             gc = gcols(t + SK + 1);
         }
         const Row nxt = row_of(t + 1);
+        // the flags the next samples' need() checks, read under this sample's LDS round trip
+        // (a need() that finds its cached counts short reads the flag and waits for every LDS
+        // read in flight: with the tagger a few rows ahead, that happened every few samples)
+        const unsigned ld_pre = TAIL ? __hip_atomic_load(&hdr->loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0u;
+        const unsigned tg_pre = __hip_atomic_load(&hdr->tagged, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __builtin_amdgcn_sched_barrier(0);
         T w0 = l0, w1 = l1;
         if constexpr (TAIL) {
@@ -646,6 +655,8 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
         }
         publish(&hdr->done, t + 1);
         cur = nxt;
+        if constexpr (TAIL) loaded = ld_pre > loaded ? ld_pre : loaded;
+        tagged = tg_pre > tagged ? tg_pre : tagged;
     };
     for (int32_t t = 0; ok && !brk && t < n_pad; t += GS)
         static_for<GS>([&](auto qc) { sample(qc, t + decltype(qc)::value); });
