@@ -59,6 +59,9 @@ constexpr int LCAP = 128;                  // entries per row (two per lane)
 #define PSGD_LDS_TB 4                      // rows per tagger step (their LDS round trips overlap;
                                            // 8 measured round 5: c4 fp32 28.9 -> 43.3 ms, fp64 56.9 -> 58.0)
 #endif
+#ifndef PSGD_LDS_NT
+#define PSGD_LDS_NT 1                      // the loader's CSR entry loads are non-temporal
+#endif
 #ifndef PSGD_LDS_EXP
 #define PSGD_LDS_EXP 0                     // cost probes (tools/r03_c4_probe.sh); 0 in the product
 #endif
@@ -298,10 +301,12 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
                 const int64_t b = rl64(bt.rb, i0 + q), e = rl64(bt.re, i0 + q);
                 const int64_t ka = b + lane, kc = b + 64 + lane;
                 const bool ia = ka < e, ic = kc < e;
-                G.ca[q] = *(ia ? &COL[ka] : dummy_i);
-                G.xa[q] = *(ia ? &X[ka] : dummy_s);
-                G.cb[q] = *(ic ? &COL[kc] : dummy_i);
-                G.xb[q] = *(ic ? &X[kc] : dummy_s);
+                // (non-temporal: the row stream is read once and must not evict the chains'
+                // L2-resident tails, ~3.2 MB per XCD in its 4 MiB at c4)
+                G.ca[q] = PSGD_LDS_NT ? __builtin_nontemporal_load(ia ? &COL[ka] : dummy_i) : *(ia ? &COL[ka] : dummy_i);
+                G.xa[q] = PSGD_LDS_NT ? __builtin_nontemporal_load(ia ? &X[ka] : dummy_s) : *(ia ? &X[ka] : dummy_s);
+                G.cb[q] = PSGD_LDS_NT ? __builtin_nontemporal_load(ic ? &COL[kc] : dummy_i) : *(ic ? &COL[kc] : dummy_i);
+                G.xb[q] = PSGD_LDS_NT ? __builtin_nontemporal_load(ic ? &X[kc] : dummy_s) : *(ic ? &X[kc] : dummy_s);
                 G.ia[q] = ia;
                 G.ic[q] = ic;
             }
