@@ -586,11 +586,12 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
         T w0 = l0, w1 = l1;
         if constexpr (TAIL) {
             // row t's gather: issued SK samples ago, followed by 4 SK VMEM instructions
-            // (PSGD_STAMPS: the time this wait takes is the chain's "wait" counter)
-            uint64_t vm0 = 0;
-            if (L.stamps) vm0 = __builtin_amdgcn_s_memtime();
+            // (-DPSGD_STAMPS builds: the time this wait takes joins the chain's "wait" counter;
+            // compiled out of the product: an s_memtime on any path into the arithmetic below
+            // makes the compiler wait for every LDS read in flight, the next row's prefetch too)
+            PSGD_STAMP(uint64_t vm0 = 0; if (L.stamps) vm0 = __builtin_amdgcn_s_memtime();)
             asm volatile("s_waitcnt vmcnt(%2)" : "+v"(gr[Q][0]), "+v"(gr[Q][1]) : "i"(4 * SK) : "memory");
-            if (L.stamps) st_wait += __builtin_amdgcn_s_memtime() - vm0;
+            PSGD_STAMP(if (L.stamps) st_wait += __builtin_amdgcn_s_memtime() - vm0;)
             // head: W[j]; tail also in rows t-SK .. t-1: that row's new value; else the gather
             w0 = r0 == kLdsDummy ? gr[Q][0] : l0;
             w1 = r1 == kLdsDummy ? gr[Q][1] : l1;
