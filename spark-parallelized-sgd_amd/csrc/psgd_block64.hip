@@ -25,8 +25,8 @@
 //     ||w - w'||^2   = b^2 ||w||^2 + c (c q - 2 b z),   b = s lambda (= 1 - a)
 // and the test sqrt(D) < tol max(sqrt(N), 1) is D < tol^2 max(N, 1). ||w||^2 starts exact (the
 // chain waves' partial norms of w_in) and follows these affine maps in the chain's sample order:
-// round 5 evaluates a block's 8 tests at once after its recurrence (a segmented scan over the
-// rows' maps, block64's CONV section), not row by row on the recurrence's dependent path. Every
+// round 5 evaluates a block's 8 tests at once after its recurrence (a scan over the rows' maps
+// in lane registers, block64's CONV section), not row by row on the recurrence's dependent path. Every
 // fp64 kernel decides as the oracle down to tol = r (1 +- 1e-13) (tests/test_gpu_break_margin.py).
 // The first row that passes ends the chain: the updates of the block's later rows, issued
 // interleaved with the recurrence, are undone (W restored from the block start, the taken rows
@@ -121,16 +121,6 @@ __host__ __device__ constexpr int row_lane64(int i) {
     return 32 * (i & 1) + 16 * ((i >> 1) & 1) + 8 * ((i >> 2) & 1);
 }
 
-// Lane `addr / 4`'s value (ds_bpermute on both halves).
-__device__ __forceinline__ double bperm_d(double v, int addr) {
-    const int lo = __builtin_amdgcn_ds_bpermute(addr, (int)lo32(v));
-    const int hi = __builtin_amdgcn_ds_bpermute(addr, (int)hi32(v));
-    return mk64((unsigned)lo, (unsigned)hi);
-}
-// The value of the lane `sh` below inside a row of 16 (DPP row_shr; 0 past the row's start).
-__device__ __forceinline__ double dpp_shr(double v, int sh) {
-    return sh == 1 ? dpp_mov<0x111>(v) : sh == 2 ? dpp_mov<0x112>(v) : dpp_mov<0x114>(v);
-}
 
 #ifndef PSGD_B64_FAST_SIGMOID
 #define PSGD_B64_FAST_SIGMOID 1
@@ -575,6 +565,61 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
             unpack<S, double>(xraw[k][u], out);
         }
     };
+    // CONV: isConverged(w_k, w_{k+1}) (PSGD.scala:262, :333-335) for a block's rows at once:
+    // with w' = a w + c x, z = x . w (zf: the row's dot before its step) and q = x . x,
+    // ||w_{k+1}||^2 = a^2 ||w_k||^2 + c (2 a z + c q) is an affine map of ||w_k||^2 per row and
+    // D_k = ||w_k - w_{k+1}||^2 = b^2 N_k + c (c q - 2 b z) with b = s lambda. A scan over the rows'
+    // maps in k order gives N_k and N_{k+1} from the block start's norm n0, and the first row with
+    // D_k < tol^2 max(N_{k+1}, 1) ends the chain. Every lane has its own row's terms (krow): the
+    // scan is the kpair butterfly across the rows' lane groups, in registers. (Round 4 ran the test
+    // per row, ~10 dependent f64 operations on the chain waves: c2 fp64 +51 % over tol 0; the first
+    // round-5 form moved the rows' terms with ds_bpermute for a DPP segmented scan.) Returns the
+    // ballot of the passing rows (lanes 8g, ballot_rows) and sets nsq_out to N after the block.
+    auto conv_test = [&](double c_, double zf, double q, double a_, double b_, bool live, double n0,
+                         double& nsq_out) __attribute__((always_inline)) -> unsigned long long {
+        const double cq1 = c_ * q;
+        double Nn, dd;
+        if constexpr (UPD == U_SQUARED_L2) {
+            // row k's map N -> A N + B; the exclusive prefix map (eA, eB) of the rows before it
+            // gives N_k, then N_{k+1} = A N_k + B and D_k = b^2 N_k + E
+            const double A = a_ * a_;
+            const double B = c_ * __builtin_fma(2.0 * a_, zf, cq1);
+            const double E = c_ * __builtin_fma(-2.0 * b_, zf, cq1);
+            double eA = 1.0, eB = 0.0, tA = A, tB = B;
+            static_for<3>([&](auto jc) {
+                constexpr int J = decltype(jc)::value;
+                const PairD pA = kpair<J>(tA, lane), pB = kpair<J>(tB, lane);
+                const bool up = (lane & kbit<J>()) != 0;   // the lower half's rows come first
+                const double nA = eA * pA.lo, nB = __builtin_fma(eA, pB.lo, eB);
+                eA = up ? nA : eA;
+                eB = up ? nB : eB;
+                if constexpr (J < 2) {
+                    tA = pA.hi * pA.lo;
+                    tB = __builtin_fma(pA.hi, pB.lo, pB.hi);
+                }
+            });
+            const double Nk = __builtin_fma(eA, n0, eB);
+            Nn = __builtin_fma(A, Nk, B);
+            dd = __builtin_fma(b_ * b_, Nk, E);
+        } else {
+            // N_{k+1} = n0 + the inclusive sum of B over the rows up to k
+            double incl = c_ * __builtin_fma(2.0, zf, cq1), tot = incl;
+            dd = c_ * cq1;
+            static_for<3>([&](auto jc) {
+                constexpr int J = decltype(jc)::value;
+                const PairD p = kpair<J>(tot, lane);
+                incl = (lane & kbit<J>()) ? p.lo + incl : incl;
+                if constexpr (J < 2) tot = p.lo + p.hi;
+            });
+            Nn = n0 + incl;
+        }
+        // one lane per row (l & 7 == 0) decides it; rows >= kk carry no step and never pass
+        const bool pass = ((lane & 7) == 0) & live & (dd < tol2 * (Nn > 1.0 ? Nn : 1.0));   // branch-free
+        const double nb = readlane_d(Nn, row_lane64(kB - 1));   // rows >= kk are identities
+        nsq_out = nb > 0.0 ? nb : 0.0;
+        return __builtin_amdgcn_ballot_w64(pass);
+    };
+    double wsave[CONV ? EH : 1];   // CONV: W at the block start (a pass restores it)
     // One block of kk rows (kB unless TAIL), rows in registers.
     auto block = [&](auto tail_c, int64_t b, int kk) __attribute__((always_inline)) -> bool {
         constexpr bool TAIL = decltype(tail_c)::value;
@@ -711,7 +756,6 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
         // at the block start (the updates run interleaved with the recurrence, before the block's
         // break test; a break -- once per chain -- restores W and replays the rows it takes)
         double ck = 0.0;
-        double wsave[(CONV && PSGD_B64_INTERLEAVE) ? EH : 1];
         if constexpr (CONV && PSGD_B64_INTERLEAVE) {
 #pragma unroll
             for (int e = 0; e < EH; ++e) wsave[e] = w[e];
@@ -721,7 +765,9 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
             const double cv = coef64<GRAD>(z, yv, nsv);
             c[i] = readlane_d(cv, row_lane64(i));
             if constexpr (TAIL) c[i] = i < kk ? c[i] : 0.0;
-            if constexpr (CONV) ck = krow == i ? cv : ck;
+            // (Logistic: this lane's coefficient as computed at its row's step; the cheap
+            // multipliers are recomputed once after the recurrence from the same z)
+            if constexpr (CONV && GRAD == G_LOGISTIC) ck = krow == i ? cv : ck;
             if constexpr (UPD == U_SQUARED_L2) {
                 al[i] = readlane_d(alpha, row_lane64(i));
                 if constexpr (TAIL) al[i] = i < kk ? al[i] : 1.0;
@@ -737,72 +783,37 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
             if constexpr (PSGD_B64_INTERLEAVE) update_row(i);
         }
         if constexpr (UPD != U_SQUARED_L2) zf = z;
+        // (a lane's z stops moving after its row's step: G[k][i] = 0 for i >= k; SquaredL2's zf
+        // keeps it through the later rows' shrinks)
+        if constexpr (CONV && GRAD != G_LOGISTIC) ck = coef64<GRAD>(zf, yv, nsv);
         if constexpr (CONV) {
-            // isConverged(w_k, w_{k+1}) (PSGD.scala:262, :333-335) for the block's rows at once:
-            // with w' = a w + c x, z = x . w (zf: the row's dot before its step) and q = x . x,
-            // ||w_{k+1}||^2 = a^2 ||w_k||^2 + c (2 a z + c q) is an affine map of ||w_k||^2 per row
-            // and D_k = ||w_k - w_{k+1}||^2 = b^2 N_k + c (c q - 2 b z) with b = s lambda. The
-            // rows' terms move to lanes 8m + k (ds_bpermute), a segmented scan over each 8-lane
-            // group (DPP row_shr 1, 2, 4) gives N_k and N_{k+1} from the block start's norm, and the
-            // first row with D_k < tol^2 max(N_{k+1}, 1) ends the chain. (Round 4 ran the test per
-            // row, ~10 dependent f64 operations on the chain waves: c2 fp64 +51 % over tol 0.)
+            // isConverged for the block's rows at once (conv_test)
             const bool live = !TAIL || krow < kk;
             const double c_ = live ? ck : 0.0;
-            const double cq1 = c_ * q;
-            const int kl = lane & 7;                        // the row this lane carries below
-            const int src = row_lane64(kl) * 4;             // a lane of row kl (bpermute address)
-            double Nn, dd;
-            if constexpr (UPD == U_SQUARED_L2) {
-                const double a_ = live ? alpha : 1.0, b_ = sv * lam;
-                double A = bperm_d(a_ * a_, src);
-                double B = bperm_d(c_ * __builtin_fma(2.0 * a_, zf, cq1), src);
-                const double b2 = bperm_d(b_ * b_, src);
-                const double E = bperm_d(c_ * __builtin_fma(-2.0 * b_, zf, cq1), src);
-#pragma unroll
-                for (int sh = 1; sh < kB; sh *= 2) {   // (this after the earlier one)
-                    const double oA = dpp_shr(A, sh), oB = dpp_shr(B, sh);
-                    const bool take = kl >= sh;
-                    const double nB = __builtin_fma(A, oB, B);
-                    A = take ? A * oA : A;
-                    B = take ? nB : B;
-                }
-                Nn = __builtin_fma(A, nsq, B);
-                double Nk = dpp_shr(Nn, 1);
-                Nk = kl == 0 ? nsq : Nk;
-                dd = __builtin_fma(b2, Nk, E);
-            } else {
-                double B = bperm_d(c_ * __builtin_fma(2.0, zf, cq1), src);
-                dd = bperm_d(c_ * cq1, src);
-#pragma unroll
-                for (int sh = 1; sh < kB; sh *= 2) {
-                    const double oB = dpp_shr(B, sh);
-                    B = kl >= sh ? oB + B : B;
-                }
-                Nn = nsq + B;
-            }
-            // lanes 0 .. 7 decide rows 0 .. 7 (rows >= kk carry no step and never pass)
-            const bool pass = (lane < kB) & (!TAIL || kl < kk) & (dd < tol2 * (Nn > 1.0 ? Nn : 1.0));   // branch-free
-            const unsigned long long m = __builtin_amdgcn_ballot_w64(pass);
-            if constexpr (PSGD_B64_INTERLEAVE) {
-                // the interleaved updates stay ahead of the test (the compiler would otherwise
-                // sink them into the no-break branch, off the recurrence they are there to fill)
-#pragma unroll
-                for (int e = 0; e < EH; ++e) asm volatile("" : "+v"(w[e]));
-            }
-            if (m != 0ull) {   // a row passed: the first one ends the chain (once per chain)
-                const int kstar = __builtin_ctzll(m);
-                brk = true;
-                keff = kstar + 1;
+            const double a_ = (UPD == U_SQUARED_L2 && live) ? alpha : 1.0, b_ = sv * lam;
+            {
+                double nb;
+                const unsigned long long m = conv_test(c_, zf, q, a_, b_, live, nsq, nb);
                 if constexpr (PSGD_B64_INTERLEAVE) {
+                    // the interleaved updates stay ahead of the test (the compiler would otherwise
+                    // sink them into the no-break branch, off the recurrence they are there to fill)
 #pragma unroll
-                    for (int e = 0; e < EH; ++e) w[e] = wsave[e];
-#pragma unroll
-                    for (int i = 0; i < kB; ++i)
-                        if (i <= kstar) update_row(i);
+                    for (int e = 0; e < EH; ++e) asm volatile("" : "+v"(w[e]));
                 }
-            } else {
-                const double nb = readlane_d(Nn, kB - 1);   // rows >= kk are identities
-                nsq = nb > 0.0 ? nb : 0.0;
+                if (m != 0ull) {   // a row passed: the first one ends the chain (once per chain)
+                    const int kstar = __builtin_ctz(ballot_rows(m));   // the first passing row
+                    brk = true;
+                    keff = kstar + 1;
+                    if constexpr (PSGD_B64_INTERLEAVE) {
+#pragma unroll
+                        for (int e = 0; e < EH; ++e) w[e] = wsave[e];
+#pragma unroll
+                        for (int i = 0; i < kB; ++i)
+                            if (i <= kstar) update_row(i);
+                    }
+                } else {
+                    nsq = nb;
+                }
             }
         }
         if (lead) {

@@ -61,6 +61,43 @@ __device__ __forceinline__ double swap_sum32(double v) {
     return e + o;
 }
 
+// The k-ordered butterfly over a block's 8 rows where the blocked kernels' transposed reductions
+// leave them (lane l carries row k(l) = l5 | l4<<1 | l3<<2): level J pairs the lanes that differ
+// in k's bit J -- lane bit 5 (permlane32_swap), 4 (permlane16_swap), 3 (DPP row_ror 8) -- and
+// returns the pair's values in k order (lo: the member with the bit clear), the same in both.
+struct PairD { double lo, hi; };
+template <int J>
+__device__ __forceinline__ PairD kpair(double v, int lane) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32);
+    auto mk = [](unsigned l, unsigned h) __attribute__((always_inline)) {
+        return __longlong_as_double((long long)(((unsigned long long)h << 32) | l));
+    };
+    if constexpr (J == 0) {
+        auto pl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+        auto ph = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+        return {mk(pl[0], ph[0]), mk(pl[1], ph[1])};
+    } else if constexpr (J == 1) {
+        auto pl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+        auto ph = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+        return {mk(pl[0], ph[0]), mk(pl[1], ph[1])};
+    } else {
+        const double p = dpp_mov<0x128>(v);   // row_ror 8: lane l ^ 8
+        return (lane & 8) ? PairD{p, v} : PairD{v, p};
+    }
+}
+// the lane bit of k's bit J
+template <int J>
+constexpr int kbit() { return J == 0 ? 32 : J == 1 ? 16 : 8; }
+// the rows (bit k) of a ballot over lanes 8g (lane 8g carries row g2 | g1<<1 | g0<<2)
+__device__ __forceinline__ unsigned ballot_rows(unsigned long long m) {
+    unsigned rows = 0;
+#pragma unroll
+    for (int g = 0; g < 8; ++g)
+        if ((m >> (8 * g)) & 1ull) rows |= 1u << (((g >> 2) & 1) | (((g >> 1) & 1) << 1) | ((g & 1) << 2));
+    return rows;
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
     v = v + dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
