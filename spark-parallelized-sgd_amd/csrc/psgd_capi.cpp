@@ -124,14 +124,35 @@ static bool contig_enabled() {
     return e && e[0] == '1';
 }
 
+// PSGD_VMM (default 1): the CSR kernels' per-chain weight vectors of 1 GiB or more are mapped
+// through the virtual memory API -- physical handles of PSGD_VMM_CHUNK_MB at a 2 GiB-aligned
+// virtual range --
+// rather than hipMalloc'd. Their scattered stores' rate depends on the placement the driver gives
+// the buffer (profiles/r05_c5_placement.log: ~65 or ~94 ms of stores per 20M c5
+// rows); mapped this way the fast placement came up in 11 of 24 measured states, hipMalloc in 1.
+static bool vmm_enabled() {
+    const char* e = getenv("PSGD_VMM");
+    return !(e && e[0] == '0');
+}
+constexpr size_t kVmmMin = size_t(1) << 30;
+constexpr size_t kVmmAlign = size_t(2) << 30;
+// the physical handles' size (PSGD_VMM_CHUNK_MB, default 2048; A/B measurements)
+static size_t vmm_chunk() {
+    const char* e = getenv("PSGD_VMM_CHUNK_MB");
+    const long mb = e && *e ? atol(e) : 2048;
+    return (size_t)(mb > 0 ? mb : 2048) << 20;
+}
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    // a virtual-memory mapping (vmm_map): the reservation and the physical handles
+    void* vres = nullptr;
+    size_t vres_bytes = 0, vmap_bytes = 0;
+    std::vector<hipMemGenericAllocationHandle_t> vh;
     hipError_t ensure(size_t need, bool contiguous = false) {
         if (need <= bytes) return hipSuccess;
-        if (p) hipFree(p);
-        p = nullptr;
-        bytes = 0;
+        release();
         hipError_t e = hipErrorOutOfMemory;
         if (contiguous && contig_enabled()) {
             e = hipExtMallocWithFlags(&p, need, hipDeviceMallocContiguous);
@@ -139,13 +160,72 @@ struct DevBuf {
                 (void)hipGetLastError();
                 p = nullptr;
             }
+        } else if (contiguous && need >= kVmmMin && vmm_enabled()) {
+            e = vmm_map(need);
+            if (e != hipSuccess) {
+                (void)hipGetLastError();
+                release();
+            }
         }
-        if (e != hipSuccess) e = hipMalloc(&p, need);
+        if (e != hipSuccess && !p) e = hipMalloc(&p, need);
         if (e == hipSuccess) bytes = need;
         return e;
     }
+    hipError_t vmm_map(size_t need) {
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e) return e;
+        hipMemAllocationProp prop = {};
+        prop.type = hipMemAllocationTypePinned;
+        prop.location.type = hipMemLocationTypeDevice;
+        prop.location.id = dev;
+        size_t gran = 0;
+        e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended);
+        if (e) return e;
+        const size_t chunk = vmm_chunk();
+        if (gran == 0 || chunk % gran || kVmmAlign % gran) return hipErrorNotSupported;
+        const size_t total = (need + gran - 1) / gran * gran;
+        // (the runtime does not honour a large alignment argument: reserve 2 GiB more and map at
+        // the first 2 GiB-aligned address inside)
+        vres_bytes = total + kVmmAlign;
+        e = hipMemAddressReserve(&vres, vres_bytes, 0, nullptr, 0);
+        if (e) {
+            vres = nullptr;
+            return e;
+        }
+        char* va = reinterpret_cast<char*>(((uintptr_t)vres + kVmmAlign - 1) / kVmmAlign * kVmmAlign);
+        for (size_t off = 0; off < total; off += chunk) {
+            const size_t sz = std::min(chunk, total - off);
+            hipMemGenericAllocationHandle_t h;
+            e = hipMemCreate(&h, sz, &prop, 0);
+            if (e) return e;
+            vh.push_back(h);
+            e = hipMemMap(va + off, sz, 0, h, 0);
+            if (e) return e;
+            vmap_bytes = off + sz;
+        }
+        hipMemAccessDesc acc = {};
+        acc.location = prop.location;
+        acc.flags = hipMemAccessFlagsProtReadWrite;
+        e = hipMemSetAccess(va, total, &acc, 1);
+        if (e) return e;
+        p = va;
+        return hipSuccess;
+    }
     void release() {
-        if (p) hipFree(p);
+        if (vres) {
+            if (vmap_bytes) {
+                const uintptr_t va = ((uintptr_t)vres + kVmmAlign - 1) / kVmmAlign * kVmmAlign;
+                hipMemUnmap(reinterpret_cast<void*>(va), vmap_bytes);
+            }
+            for (auto h : vh) hipMemRelease(h);
+            hipMemAddressFree(vres, vres_bytes);
+        } else if (p) {
+            hipFree(p);
+        }
+        vh.clear();
+        vres = nullptr;
+        vres_bytes = vmap_bytes = 0;
         p = nullptr;
         bytes = 0;
     }

@@ -207,6 +207,30 @@ __global__ __launch_bounds__(128) void ldsvar(ChainLaunch L, RingGeom geom) {
     }
 }
 
+// the buffer through the virtual memory API: 2 GiB handles at a 2 GiB-aligned range (libpsgd's
+// DevBuf::vmm_map for the CSR weight vectors)
+static void* vmm_alloc(size_t bytes) {
+    const size_t chunk = size_t(2) << 30;
+    hipMemAllocationProp prop = {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = 0;
+    const size_t total = (bytes + chunk - 1) / chunk * chunk;
+    void* res;
+    CK(hipMemAddressReserve(&res, total + chunk, 0, nullptr, 0));
+    char* va = (char*)(((uintptr_t)res + chunk - 1) / chunk * chunk);
+    for (size_t off = 0; off < total; off += chunk) {
+        hipMemGenericAllocationHandle_t h;
+        CK(hipMemCreate(&h, chunk, &prop, 0));
+        CK(hipMemMap(va + off, chunk, 0, h, 0));
+    }
+    hipMemAccessDesc acc = {};
+    acc.location = prop.location;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    CK(hipMemSetAccess(va, total, &acc, 1));
+    return va;
+}
+
 int main(int argc, char** argv) {
     const int64_t rows = argc > 1 ? atoll(argv[1]) : 39062;
     const int P = argc > 2 ? atoi(argv[2]) : 256;
@@ -216,7 +240,8 @@ int main(int argc, char** argv) {
     const int64_t rowbytes = nv * 1024;
     const size_t bytes = (size_t)rows * P * rowbytes;
     // [6] GB allocated, written and freed before the stream's buffer (a process that ran another
-    // workload first); [7] 1: the stream's buffer from hipExtMallocWithFlags(hipDeviceMallocContiguous)
+    // workload first); [7] 1: the stream's buffer from hipExtMallocWithFlags(hipDeviceMallocContiguous),
+    // 2: mapped through the virtual memory API (vmm_alloc)
     const double pre_gb = argc > 6 ? atof(argv[6]) : 0.0;
     const int contig = argc > 7 ? atoi(argv[7]) : 0;
     if (pre_gb > 0) {
@@ -228,7 +253,10 @@ int main(int argc, char** argv) {
         CK(hipFree(T));
     }
     void* X;
-    if (contig) {
+    if (contig == 2) {
+        X = vmm_alloc(bytes);
+        printf("vmm mapping of %.1f GB at %p\n", bytes / 1e9, X);
+    } else if (contig) {
         hipError_t e = hipExtMallocWithFlags(&X, bytes, hipDeviceMallocContiguous);
         printf("contiguous allocation of %.1f GB: %s\n", bytes / 1e9, hipGetErrorString(e));
         if (e != hipSuccess) { (void)hipGetLastError(); CK(hipMalloc(&X, bytes)); }
