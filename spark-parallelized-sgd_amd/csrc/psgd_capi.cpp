@@ -134,7 +134,12 @@ static bool vmm_enabled() {
     const char* e = getenv("PSGD_VMM");
     return !(e && e[0] == '0');
 }
-constexpr size_t kVmmMin = size_t(1) << 30;
+// (PSGD_VMM_MIN_MB: the smallest set mapped this way, default 1024; A/B measurements)
+static size_t vmm_min() {
+    const char* e = getenv("PSGD_VMM_MIN_MB");
+    const long mb = e && *e ? atol(e) : 1024;
+    return (size_t)(mb >= 0 ? mb : 1024) << 20;
+}
 constexpr size_t kVmmAlign = size_t(2) << 30;
 // the physical handles' size (PSGD_VMM_CHUNK_MB, default 2048; A/B measurements)
 static size_t vmm_chunk() {
@@ -160,7 +165,7 @@ struct DevBuf {
                 (void)hipGetLastError();
                 p = nullptr;
             }
-        } else if (contiguous && need >= kVmmMin && vmm_enabled()) {
+        } else if (contiguous && need >= vmm_min() && vmm_enabled()) {
             e = vmm_map(need);
             if (e != hipSuccess) {
                 (void)hipGetLastError();
