@@ -779,7 +779,9 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
                 if (i + 1 < kB) z = __builtin_fma(c[i], G[i], z);
             }
             // row i's update is independent of the next coefficient's dependent chain: issued
-            // here, it fills that chain's latency (PSGD_B64_INTERLEAVE=0: after the recurrence)
+            // here, it fills that chain's latency (PSGD_B64_INTERLEAVE=0: after the recurrence;
+            // pinning each row's update before the next step with an empty asm measured no gain,
+            // r05: c3 Logistic f32 rows 488 -> 492 cycles per row, c2 LeastSquares 239 -> 242)
             if constexpr (PSGD_B64_INTERLEAVE) update_row(i);
         }
         if constexpr (UPD != U_SQUARED_L2) zf = z;
@@ -864,6 +866,9 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
         unsigned long long* o = L.stamps + (size_t)chain * 16;
         o[0] = __builtin_amdgcn_s_memtime() - st_begin; o[1] = st_rd; o[2] = st_gr;
         o[3] = st_p; o[7] = st_x; o[12 + 2] = st_rec; o[12 + 3] = st_upd;
+    } else if (L.stamps && H == 2 && lane == 0) {
+        unsigned long long* o = L.stamps + (size_t)chain * 16;
+        o[10] = st_x; o[11] = st_p;   // the second chain wave's exchange wait and dots
     })
     loss_sum = wave_sum(loss_sum);   // the 8 loss lanes' partials
 

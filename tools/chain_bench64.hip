@@ -133,7 +133,7 @@ int main(int argc, char** argv) {
            best * 1e6 / rows, w);
     const char* names[16] = {"chain.total", "chain.wait_rows", "chain.wait_gram", "chain.p+reduce",
                              "loader.total", "loader.ring_full", "loader.vmcnt", "chain.wait_xchg",
-                             "gram0.total", "gram0.wait_rows", "-", "-",
+                             "gram0.total", "gram0.wait_rows", "chain1.wait_xchg", "chain1.p+reduce",
                              "gram1.total", "gram1.wait_rows", "chain.recurrence", "chain.loss+update"};
     for (int k = 0; k < 16; ++k) {
         if (names[k][0] == '-') continue;
