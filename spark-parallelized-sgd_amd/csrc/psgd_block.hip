@@ -486,13 +486,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         float zf = z;
         bool brk = false;   // CONV: a row of this block passed isConverged
         int keff = kk;      // the rows taken
-        float ck = 0.0f;    // CONV: this lane's row's coefficient (lane row_lane(k) computes c_k at step k)
+        float ck = 0.0f;    // CONV: this lane's row's coefficient (lane row_lane(k) computed c_k at step k)
 #pragma unroll
         for (int i = 0; i < kBlk; ++i) {
             const float cv = coef<GRAD>(z, yv, sv, nsv, aux);
             c[i] = readlane_f(cv, row_lane(i));
             if constexpr (TAIL) c[i] = i < kk ? c[i] : 0.0f;
-            if constexpr (CONV) ck = krow == i ? cv : ck;
             if constexpr (UPD == U_SQUARED_L2) {
                 al[i] = readlane_f(alpha, row_lane(i));
                 if constexpr (TAIL) al[i] = i < kk ? al[i] : 1.0f;
@@ -505,6 +504,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             }
         }
         if constexpr (UPD != U_SQUARED_L2) zf = z;
+        // CONV: this lane's row's coefficient, recomputed once from its final z (a lane's z stops
+        // moving after its row's step: G[k][i] = 0 for i >= k; SquaredL2's zf keeps it through
+        // the later rows' shrinks) -- the value row_lane(k) computed at step k, for ~3 operations
+        // instead of a select at each of the 8 steps
+        if constexpr (CONV) ck = coef<GRAD>(zf, yv, sv, nsv, aux);
         // W <- a_i W + c_i x_i for the block's rows in sample order (CONV: every row, as if no
         // row passes; W at the block start is kept for the rare block where one does)
         auto update_rows = [&](int last) __attribute__((always_inline)) {
