@@ -793,29 +793,27 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
             const bool live = !TAIL || krow < kk;
             const double c_ = live ? ck : 0.0;
             const double a_ = (UPD == U_SQUARED_L2 && live) ? alpha : 1.0, b_ = sv * lam;
-            {
-                double nb;
-                const unsigned long long m = conv_test(c_, zf, q, a_, b_, live, nsq, nb);
+            double nb;
+            const unsigned long long m = conv_test(c_, zf, q, a_, b_, live, nsq, nb);
+            if constexpr (PSGD_B64_INTERLEAVE) {
+                // the interleaved updates stay ahead of the test (the compiler would otherwise
+                // sink them into the no-break branch, off the recurrence they are there to fill)
+#pragma unroll
+                for (int e = 0; e < EH; ++e) asm volatile("" : "+v"(w[e]));
+            }
+            if (m != 0ull) {   // a row passed: the first one ends the chain (once per chain)
+                const int kstar = __builtin_ctz(ballot_rows(m));   // the first passing row
+                brk = true;
+                keff = kstar + 1;
                 if constexpr (PSGD_B64_INTERLEAVE) {
-                    // the interleaved updates stay ahead of the test (the compiler would otherwise
-                    // sink them into the no-break branch, off the recurrence they are there to fill)
 #pragma unroll
-                    for (int e = 0; e < EH; ++e) asm volatile("" : "+v"(w[e]));
+                    for (int e = 0; e < EH; ++e) w[e] = wsave[e];
+#pragma unroll
+                    for (int i = 0; i < kB; ++i)
+                        if (i <= kstar) update_row(i);
                 }
-                if (m != 0ull) {   // a row passed: the first one ends the chain (once per chain)
-                    const int kstar = __builtin_ctz(ballot_rows(m));   // the first passing row
-                    brk = true;
-                    keff = kstar + 1;
-                    if constexpr (PSGD_B64_INTERLEAVE) {
-#pragma unroll
-                        for (int e = 0; e < EH; ++e) w[e] = wsave[e];
-#pragma unroll
-                        for (int i = 0; i < kB; ++i)
-                            if (i <= kstar) update_row(i);
-                    }
-                } else {
-                    nsq = nb;
-                }
+            } else {
+                nsq = nb;
             }
         }
         if (lead) {
