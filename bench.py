@@ -48,6 +48,11 @@ SECONDARY_ROWS = {"c5": 20_000_000}
 # turns NaN once the squared-gradient average r exceeds 1, which least squares at c2 reaches)
 DEFAULT_SECONDARY = ("c3:f32,c3:f64::f64,c3:f64,c2:f64,c1:f64,c4:f32,c4:f64,c4:f64::f64,c5:f32,c5:f64,"
                      "c3:f32:adagrad,c3:f32:adam,c3:f64:adagrad,c3:f64:adam")
+# N > 1 (the driver's scaling runs): BASELINE's own multi-GPU configs as secondaries, per GPU --
+# configs[2] (dense logistic 100M x 1024 over 8 GPUs = c3's 12.5M-row shard per GPU, fp32 and the
+# reference's f64 rows) and configs[4] (1B-row L2 logistic over 8 GPUs = c5's full 125M-row shard)
+DEFAULT_SECONDARY_MULTI = "c3:f32,c3:f64::f64,c5:f32"
+SECONDARY_ROWS_MULTI = {"c5": 125_000_000}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
@@ -162,8 +167,11 @@ def parse():
                     help="miniBatchFraction: batch i = RDD.sample(false, f, 42 + i) per partition")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--secondary", default=DEFAULT_SECONDARY,
-                    help="comma list of workload[:compute[:updater]] measured after the headline (1 GPU only; '' = none)")
+    ap.add_argument("--secondary", default=None,
+                    help="comma list of workload[:compute[:updater[:storage]]] measured after the headline "
+                         "(default: DEFAULT_SECONDARY on 1 GPU, DEFAULT_SECONDARY_MULTI on N > 1; '' = none)")
+    ap.add_argument("--secondary-rows", type=int, default=0,
+                    help="rows per GPU of every secondary workload (testing; 0 = each workload's default)")
     ap.add_argument("--updater", default="", help="another SGDUpdater for the headline workload (experiments)")
     ap.add_argument("--storage", default="", choices=["", "f32", "f64"],
                     help="row storage dtype of the headline workload (default: the workload's own)")
@@ -485,6 +493,8 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
     torch.cuda.synchronize()
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(steps)]
+    if world > 1:
+        engine.exchange_events = []   # HIP events around each timed step's all-gather + fold
     t0 = time.perf_counter()
     total = 0
     for i in range(steps):
@@ -510,6 +520,17 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
     epoch_ms = [a.elapsed_time(b) for a, b in events]
     avg_epoch_s = sum(epoch_ms) / len(epoch_ms) / 1e3
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+    ranks = None
+    if world > 1:
+        # every rank's chain-kernel ms and all-gather + fold ms (its HIP events), gathered to all
+        xchg = [a.elapsed_time(b) for a, b in engine.exchange_events]
+        engine.exchange_events = None
+        mine = torch.tensor([avg_kernel_s * 1e3, sum(xchg) / max(len(xchg), 1)], dtype=torch.float64,
+                            device=red_dev)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        ranks = {"kernel_ms": [round(float(t[0]), 3) for t in allr],
+                 "xchg_ms": [round(float(t[1]), 4) for t in allr]}
     es = 4 if sdt == "f32" else 8
     variant = engine.ctx.last_kernel()
     offchip = None
@@ -528,15 +549,12 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
     local_samples = n if fraction >= 1.0 and tol == 0.0 else samples_per_step / world
     # one chain-kernel launch processes every (sampled) row of this GPU's partitions
     achieved = local_samples * bytes_per_sample / avg_kernel_s / 1e9
+    # the step-level figure beside the kernel's: per-GPU samples/s of the driver-timed step x B
+    frac_step = value / world * bytes_per_sample / 1e9 / HBM_PEAK_GBS
     upd_name = updater or ("squared_l2" if reg > 0 else "simple")
     traffic, traffic_src = pmc_traffic(workload, grad, variant, sdt, n, compute, upd_name)
-    note = None
-    if compute == "f32" and workload == "c3" and not updater:
-        note = ("fp32 compute at C3's step 1.0 is a throughput mode without a uniform weight tolerance "
-                "(DESIGN.md §4); the parity claims for C3 are the fp64 lines")
     res = {
         "value": value, "ms_per_step": elapsed / steps * 1e3, "dtype": compute, "loss": loss,
-        **({"precision_note": note} if note else {}),
         "config": {"workload": f"{workload}: {cfg_name}", "rows_per_gpu": n, "d": d,
                    "chains_per_gpu": P, "storage": sdt, "gradient": grad,
                    "updater": updater or ("squared_l2" if reg > 0 else "simple"), "reg_param": reg,
@@ -545,7 +563,7 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
                                                    if backend == "nccl" else
                                                    " (chains sharded, gloo all-gather + fold per epoch: a rehearsal)")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS, "frac_step": frac_step, "traffic": traffic,
                      "traffic_source": traffic_src,
                      "kernel": kernel_name(variant),
                      "bytes_per_launch": local_samples * bytes_per_sample,
@@ -560,12 +578,50 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
                      "variant": variant,
                      "timing": "HIP events recorded around each chain-kernel launch on its stream"},
         "prewarm": {"seconds": prewarm_s, "epochs": prewarm_epochs},   # untimed, model discarded
+        **({"ranks": ranks} if ranks else {}),
         "_meta": (grad, d, P, step, csr, upd_name, reg),
         # per timed step, the chain kernel's ms (the detail file only; the stdout line drops it)
         "kernel_ms_series": [round(x, 4) for x in kernel_ms],
     }
+    if workload == "c5" and csr:
+        res["c5_store_probe"] = c5_store_probe(torch, pkg, engine, params, w0, parts, all_parts, empty,
+                                               rank, P)
     del engine, data, parts, all_parts
     return res
+
+
+# c5's kernel time follows the write rate of its scattered stores over the chains' weight vectors,
+# which takes one of two levels decided by the physical placement the vectors' allocation received
+# (profiles/r05_c5_placement.log). The probe times the same kernel over the first
+# C5_PROBE_ROWS rows of every chain, on the same (reused) vector allocation, so box-to-box c5
+# numbers can be read against the mode the run landed in. The threshold is the measured gap
+# between the two levels.
+C5_PROBE_ROWS = 2000
+C5_PROBE_FAST_NS = {"f32": 4.7, "f64": 5.0}   # ns per row at or below: the fast store mode
+
+
+def c5_store_probe(torch, pkg, engine, params, w, parts, all_parts, empty, rank, P):
+    probe = [None] * len(all_parts)
+    for p, part in enumerate(parts):
+        m = min(C5_PROBE_ROWS, part.n_rows)
+        probe[rank * P + p] = pkg.DeviceCsrPartition(part.labels[:m], part.row_ptr[:m + 1], part.col,
+                                                     part.val, part.d)
+    for i in range(len(probe)):
+        if probe[i] is None:
+            probe[i] = empty()
+    eng = pkg.HipEngine(pkg.PartitionedData(probe), engine.rank, engine.world, device=engine.device)
+    ms = []
+    for _ in range(3):   # the chains only (no collective): this rank's placement
+        with torch.cuda.stream(eng.stream):
+            eng.local_partial(params, w, False)
+        ms.append(eng.ctx.last_chain_ms())
+    rows = sum(min(C5_PROBE_ROWS, part.n_rows) for part in parts)
+    best = min(ms[1:])
+    ns = best * 1e6 / max(rows, 1)
+    comp = "f32" if params.compute_dtype == pkg._native.F32 else "f64"
+    del eng
+    return {"rows_per_chain": C5_PROBE_ROWS, "ms": round(best, 4), "ns_per_row": round(ns, 3),
+            "mode": "fast" if ns <= C5_PROBE_FAST_NS[comp] else "slow"}
 
 
 def main():
@@ -605,13 +661,19 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    secondary = [s for s in args.secondary.split(",") if s] if world == 1 else []
+    spec_list = args.secondary if args.secondary is not None else \
+        (DEFAULT_SECONDARY if world == 1 else DEFAULT_SECONDARY_MULTI)
+    secondary = [s for s in spec_list.split(",") if s]
+    sec_rows = SECONDARY_ROWS if world == 1 else SECONDARY_ROWS_MULTI
+
+    def rows_of(wl):
+        return args.secondary_rows or sec_rows.get(wl, 0)
     arena = None
     if not args.no_arena:
         need = shard_bytes(args.workload, args.storage, args.rows, args.features, args.skew_rows, args.chains)
         for spec in secondary:
             wl, _, _, sto = (spec.split(":") + ["", "", ""])[:4]
-            need = max(need, shard_bytes(wl, sto, SECONDARY_ROWS.get(wl, 0)))
+            need = max(need, shard_bytes(wl, sto, rows_of(wl)))
         arena = Arena(torch, dev, need)
     res = run_workload(torch, dist, pkg, dev, rank, world, local, args.workload, args.compute,
                        args.rows, args.fraction, args.steps, args.warmup, args.prewarm_s, args.features,
@@ -627,6 +689,7 @@ def main():
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": res["dtype"], "data": "synthetic (device-generated, resident in HBM)",
         "config": res["config"], "roofline": res["roofline"], "prewarm": res["prewarm"],
+        **({"ranks": res["ranks"]} if "ranks" in res else {}),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(grad, d, P, step, args.cpu_seconds,
@@ -645,7 +708,7 @@ def main():
             arena.reset()   # the previous workload's rows are dead: the next one reuses the memory
         try:
             r = run_workload(torch, dist, pkg, dev, rank, world, local, wl, comp or "f32",
-                             SECONDARY_ROWS.get(wl, 0), 1.0, args.steps, args.warmup,
+                             rows_of(wl), 1.0, args.steps, args.warmup,
                              min(args.prewarm_s, 0.5), updater=upd, storage=sto, arena=arena)
         except Exception as e:   # a secondary line never hides the headline
             records.append({"spec": spec, "error": f"{type(e).__name__}: {e}"})
@@ -672,9 +735,13 @@ def secondary_summary(records):
     """One compact entry per secondary workload: what the driver's line carries."""
     return [{"spec": r["spec"], "error": r["error"][:200]} if "error" in r else
             {"spec": r["spec"], "samples_per_s": round(r["samples_per_s"]),
-             "frac": round(r["roofline"]["frac"], 4), "kernel_ms": round(r["roofline"]["avg_kernel_ms"], 3),
+             "frac": round(r["roofline"]["frac"], 4),
+             **({"frac_step": round(r["roofline"]["frac_step"], 4)} if "frac_step" in r["roofline"] else {}),
+             "kernel_ms": round(r["roofline"]["avg_kernel_ms"], 3),
              "B_per_sample": r["roofline"]["bytes_per_sample"],
-             "variant": r["roofline"].get("variant")}
+             "variant": r["roofline"].get("variant"),
+             **({"ranks": r["ranks"]} if "ranks" in r else {}),
+             **({"c5_store_probe": r["c5_store_probe"]} if "c5_store_probe" in r else {})}
             for r in records]
 
 
@@ -707,10 +774,11 @@ def final_line(out, records):
         line["roofline"] = {k: v for k, v in line["roofline"].items() if k not in ("kernel", "timing")}
         line["config"] = {k: v for k, v in line["config"].items() if k != "parallelism"}
         s = json.dumps(line, separators=(",", ":"))
-    if len(s) > LINE_LIMIT and records:
-        line["secondary_summary"] = [{k: v for k, v in e.items() if k in ("spec", "samples_per_s", "frac")}
-                                     for e in line["secondary_summary"]]
-        s = json.dumps(line, separators=(",", ":"))
+    for keep in (("spec", "samples_per_s", "frac", "frac_step", "ranks"), ("spec", "samples_per_s", "frac")):
+        if len(s) > LINE_LIMIT and records:
+            line["secondary_summary"] = [{k: v for k, v in e.items() if k in keep}
+                                         for e in line["secondary_summary"]]
+            s = json.dumps(line, separators=(",", ":"))
     return s
 
 

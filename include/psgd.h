@@ -187,6 +187,11 @@ int32_t psgd_ctx_last_kernel(psgd_ctx* ctx);
  * recorded around it on the launch stream (waits for that launch to finish). */
 int32_t psgd_ctx_last_chain_ms(psgd_ctx* ctx, double* ms_out);
 
+/* Diagnostics (no reference counterpart): process-wide counters of the virtual-memory mappings
+ * that hold the CSR chains' large weight vectors (PSGD_VMM): out4[0] chunks mapped, [1] chunks
+ * unmapped, [2] bytes currently mapped, [3] failed unmap / release / address-free calls. */
+int32_t psgd_vmm_stats(int64_t* out4);
+
 /* The device sampler of one partition, alone: RDD.sample(false, fraction, .) over a partition
  * of n rows whose PartitionwiseSampledRDD seed is `seed` (the partition's java.util.Random
  * nextLong, before hashSeed) [ext Spark 1.6.1 BernoulliSampler] -- the batch selection

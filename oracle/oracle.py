@@ -74,6 +74,7 @@ def lib():
         L.or_xorshift_hash_seed.restype = C.c_int64
         L.or_sample_partition.argtypes = [C.c_int64, C.c_int64, C.c_double, i32p]
         L.or_sample_partition.restype = C.c_int64
+        L.or_set_f32_chain.argtypes = [C.c_int32, C.c_int32]
         _lib = L
     return _lib
 
@@ -191,6 +192,18 @@ def ratio_trace(mat: Matrix, part_offsets, chain, gradient, updater, step, reg, 
     finally:
         lib().or_set_ratio_trace(-1, None, 0)
     return buf[:m].copy()
+
+
+def run_f32(mat: Matrix, part_offsets, gradient, updater, step, iters, reg, w0, order=0, **kw):
+    """run() with every dense Simple / SquaredL2 chain evaluated in IEEE single precision
+    (or_set_f32_chain: the sequential fp32 restatement; order 0 = left-fold dots, 1 = 64 strided
+    partials + pairwise tree, 2 = only the weights float, the dot and multiplier in double, tol = 0).
+    The driver and the combine stay in double, as on the device."""
+    lib().or_set_f32_chain(1, int(order))
+    try:
+        return run(mat, part_offsets, gradient, updater, step, iters, reg, w0, **kw)
+    finally:
+        lib().or_set_f32_chain(0, 0)
 
 
 def run_chains(mat: Matrix, part_offsets, gradient, updater, step, reg, w_in, tol=0.0,

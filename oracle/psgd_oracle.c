@@ -458,6 +458,145 @@ int or_chain(const or_matrix* m, int64_t r0, int64_t r1, const or_params* prm,
 }
 
 /* ------------------------------------------------------------------------------------------
+ * The same chain in IEEE single precision (test infrastructure: VERDICT r05 item 1, the
+ * float-arithmetic restatement that separates the fp32 trajectory's own sensitivity from a
+ * kernel defect). Dense rows, binary gradients, Simple / SquaredL2 only; every operation of
+ * chain_rows / gradient_compute / updater_compute above in the same order with float operands
+ * (w, the dot, the multiplier, the gradient and the step rounded to float), the loss and regVal
+ * accumulated in double from the float quantities. g_f32_order selects the dot's summation:
+ * 0 = F2J's left fold (ddot), 1 = 64 strided partial sums combined by a pairwise tree (a
+ * wavefront64's order) -- two equally valid fp32 evaluations of the same chain; 2 = only the
+ * weights float (dot, multiplier and step in double, each coordinate's update rounded to float
+ * once; tol = 0 only) -- the error of fp32 weight storage alone.
+ * ------------------------------------------------------------------------------------------ */
+static int g_f32 = 0, g_f32_order = 0;
+
+void or_set_f32_chain(int32_t on, int32_t order) {
+    g_f32 = on;
+    g_f32_order = order;
+}
+
+static float dot_f32(int32_t d, const float* x, const float* w) {
+    if (g_f32_order == 0) {
+        float s = 0.0f;
+        for (int32_t i = 0; i < d; ++i) s = s + x[i] * w[i];
+        return s;
+    }
+    float part[64];
+    for (int l = 0; l < 64; ++l) part[l] = 0.0f;
+    for (int32_t i = 0; i < d; ++i) part[i & 63] = part[i & 63] + x[i] * w[i];
+    for (int h = 32; h >= 1; h >>= 1)
+        for (int l = 0; l < h; ++l) part[l] = part[l] + part[l + h];
+    return part[0];
+}
+
+static int chain_rows_f32(const or_matrix* m, int64_t r0, int64_t r1, const or_params* prm,
+                          const double* w_in, double* w_out, double* rv_out, double* loss_out,
+                          int64_t* count_out) {
+    const int32_t d = m->d;
+    size_t nd = (size_t)(d > 0 ? d : 1);
+    float* buf = (float*)malloc(sizeof(float) * nd * 4);
+    if (!buf) return -1;
+    float *w = buf, *old = buf + nd, *x = buf + 2 * nd, *g = buf + 3 * nd;
+    for (int32_t i = 0; i < d; ++i) w[i] = (float)w_in[i];
+    memcpy(old, w, sizeof(float) * nd);
+    double localRegVal = 0.0, localLossSum = 0.0;
+    int64_t count = 0, j = 1;
+    for (int64_t r = r0; r < r1; ++r) {
+        const double* xr = m->X + (size_t)r * (size_t)m->ld;
+        for (int32_t i = 0; i < d; ++i) x[i] = (float)xr[i];
+        const float label = (float)m->labels[r];
+        if (g_f32_order == 2) {
+            /* order 2: only the weights are float -- dot, multiplier and step in double, each
+             * coordinate's update rounded to float once (isolates the weight-storage rounding) */
+            double dd = 0.0;
+            for (int32_t i = 0; i < d; ++i) dd = dd + (double)x[i] * (double)w[i];
+            row_t rw;
+            memset(&rw, 0, sizeof rw);
+            double mlt, ls;
+            if (prm->gradient == OR_GRAD_LOGISTIC) {
+                mlt = (1.0 / (1.0 + exp(-dd))) - m->labels[r];
+                ls = m->labels[r] > 0.0 ? log1p_exp(-dd) : log1p_exp(-dd) + dd;
+            } else if (prm->gradient == OR_GRAD_LEAST_SQUARES) {
+                mlt = dd - m->labels[r];
+                ls = mlt * mlt / 2.0;
+            } else {
+                const double ys = 2 * m->labels[r] - 1.0;
+                mlt = 1.0 > ys * dd ? -ys : 0.0;
+                ls = 1.0 > ys * dd ? 1.0 - ys * dd : 0.0;
+            }
+            const double st = prm->step_size / sqrt((double)j);
+            const double c2 = prm->updater == OR_UPD_SQUARED_L2 ? 1.0 - st * prm->reg_param : 1.0;
+            for (int32_t i = 0; i < d; ++i) w[i] = (float)((double)w[i] * c2 + (-st) * (mlt * (double)x[i]));
+            localRegVal = 0.0;
+            if (prm->updater == OR_UPD_SQUARED_L2) {
+                double s2 = 0.0;
+                for (int32_t i = 0; i < d; ++i) s2 = s2 + (double)w[i] * (double)w[i];
+                localRegVal = 0.5 * prm->reg_param * s2;
+            }
+            localLossSum += ls;
+            count += 1;
+            j += 1;
+            continue;   /* no per-sample test in this probe (tol = 0 only) */
+        }
+        const float dotv = dot_f32(d, x, w);
+        float mult;
+        double loss;
+        int dense_grad = 1;
+        if (prm->gradient == OR_GRAD_LOGISTIC) {
+            const float margin = -1.0f * dotv;
+            mult = (1.0f / (1.0f + expf(margin))) - label;
+            loss = label > 0.0f ? log1p_exp((double)margin) : log1p_exp((double)margin) - (double)margin;
+        } else if (prm->gradient == OR_GRAD_LEAST_SQUARES) {
+            mult = dotv - label;
+            loss = (double)mult * (double)mult / 2.0;
+        } else {
+            const float labelScaled = 2.0f * label - 1.0f;
+            if (1.0f > labelScaled * dotv) {
+                mult = -labelScaled;
+                loss = 1.0 - (double)labelScaled * (double)dotv;
+            } else {
+                mult = 0.0f;
+                loss = 0.0;
+                dense_grad = 0;
+            }
+        }
+        for (int32_t i = 0; i < d; ++i) g[i] = mult * x[i];
+        const float step = (float)(prm->step_size / sqrt((double)j));
+        if (prm->updater == OR_UPD_SQUARED_L2) {
+            const float c = (float)(1.0 - (double)step * prm->reg_param);
+            for (int32_t i = 0; i < d; ++i) w[i] = w[i] * c;
+        }
+        if (dense_grad)
+            for (int32_t i = 0; i < d; ++i) w[i] = w[i] + (-step) * g[i];
+        if (prm->updater == OR_UPD_SQUARED_L2) {
+            double s = 0.0;
+            for (int32_t i = 0; i < d; ++i) s = s + (double)w[i] * (double)w[i];
+            localRegVal = 0.5 * prm->reg_param * s;
+        } else {
+            localRegVal = 0.0;
+        }
+        localLossSum += loss;
+        count += 1;
+        j += 1;
+        double s = 0.0, n2 = 0.0;
+        for (int32_t i = 0; i < d; ++i) {
+            const double t = (double)old[i] - (double)w[i];
+            s = s + t * t;
+            n2 = n2 + (double)w[i] * (double)w[i];
+        }
+        if (sqrt(s) < prm->convergence_tol * jmax(sqrt(n2), 1.0)) break;
+        memcpy(old, w, sizeof(float) * nd);
+    }
+    for (int32_t i = 0; i < d; ++i) w_out[i] = (double)w[i];
+    *rv_out = localRegVal;
+    *loss_out = localLossSum;
+    *count_out = count;
+    free(buf);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------
  * Combine -- ParallelizedSGD.scala:271-276 (Breeze vector * scalar, +, / elementwise).
  * ------------------------------------------------------------------------------------------ */
 void or_combine(int32_t d, double* acc_w, double* acc_rv, double* acc_loss, int64_t* acc_c,
@@ -501,6 +640,13 @@ static void* chain_worker(void* arg) {
             r1 = r0 + jb->nrows[p];
         }
         if (jb->limits && r1 - r0 > jb->limits[p]) r1 = r0 + jb->limits[p];
+        if (g_f32 && !rows && !jb->m->is_csr && jb->prm->num_classes <= 2 &&
+            (jb->prm->updater == OR_UPD_SIMPLE || jb->prm->updater == OR_UPD_SQUARED_L2)) {
+            if (chain_rows_f32(jb->m, r0, r1, jb->prm, jb->w_in, jb->w_out + (size_t)p * (size_t)d,
+                               &jb->rv[p], &jb->loss[p], &jb->cnt[p]) != 0)
+                jb->rc = -1;
+            continue;
+        }
         if (chain_rows(jb->m, r0, r1, rows, jb->prm, jb->w_in, jb->w_out + (size_t)p * (size_t)d,
                        &jb->rv[p], &jb->loss[p], &jb->cnt[p], p) != 0)
             jb->rc = -1;

@@ -110,6 +110,14 @@ void or_set_margin_probe(double* buf, int32_t iters, int32_t P);
 void or_set_ratio_trace(int32_t chain, double* buf, int64_t cap);
 int64_t or_ratio_trace_len(void);
 
+/* fp32 restatement switch (test infrastructure): on != 0 runs dense Simple / SquaredL2 chains
+ * with binary gradients in IEEE single precision (same operations, float operands; loss and regVal
+ * accumulated in double) -- the reference of what a sequential fp32 evaluation of the chain gives.
+ * order 0: the dot as a left fold; 1: 64 strided partials + a pairwise tree; 2: only the weights
+ * in float (dot and multiplier in double, updates rounded to float; tol = 0 only). Not thread-safe
+ * across callers (one global switch); the driver and fold stay in double. */
+void or_set_f32_chain(int32_t on, int32_t order);
+
 /* RDD.sample(false, fraction, seed) [ext Spark 1.6.1]: the per-partition seeds
  * (java.util.Random(seed).nextLong() in partition order), XORShiftRandom.hashSeed, and the
  * BernoulliSampler's row selection for one partition of n rows (returns the count, writes the

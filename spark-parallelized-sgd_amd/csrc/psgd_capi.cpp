@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -148,13 +149,25 @@ static size_t vmm_chunk() {
     return (size_t)(mb > 0 ? mb : 2048) << 20;
 }
 
+// Process-wide counters of the VMM mappings (psgd_vmm_stats): chunks mapped and unmapped, bytes
+// currently mapped, and failed unmap / release / address-free calls (each also logged to stderr).
+static std::atomic<int64_t> g_vmm_mapped{0}, g_vmm_unmapped{0}, g_vmm_live_bytes{0}, g_vmm_failures{0};
+
+static void vmm_fail(const char* what, hipError_t e) {
+    g_vmm_failures.fetch_add(1);
+    fprintf(stderr, "psgd: %s failed while releasing a VMM buffer: %s\n", what, hipGetErrorString(e));
+    (void)hipGetLastError();
+}
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
-    // a virtual-memory mapping (vmm_map): the reservation and the physical handles
+    // a virtual-memory mapping (vmm_map): the reservation, the physical handles and, per handle,
+    // the (offset, size) it is mapped at inside the aligned range -- unmapped one by one, as mapped
     void* vres = nullptr;
-    size_t vres_bytes = 0, vmap_bytes = 0;
+    size_t vres_bytes = 0;
     std::vector<hipMemGenericAllocationHandle_t> vh;
+    std::vector<std::pair<size_t, size_t>> vmaps;
     hipError_t ensure(size_t need, bool contiguous = false) {
         if (need <= bytes) return hipSuccess;
         release();
@@ -175,6 +188,9 @@ struct DevBuf {
         if (e != hipSuccess && !p) e = hipMalloc(&p, need);
         if (e == hipSuccess) bytes = need;
         return e;
+    }
+    char* vmm_base() const {
+        return reinterpret_cast<char*>(((uintptr_t)vres + kVmmAlign - 1) / kVmmAlign * kVmmAlign);
     }
     hipError_t vmm_map(size_t need) {
         int dev = 0;
@@ -198,7 +214,7 @@ struct DevBuf {
             vres = nullptr;
             return e;
         }
-        char* va = reinterpret_cast<char*>(((uintptr_t)vres + kVmmAlign - 1) / kVmmAlign * kVmmAlign);
+        char* va = vmm_base();
         for (size_t off = 0; off < total; off += chunk) {
             const size_t sz = std::min(chunk, total - off);
             hipMemGenericAllocationHandle_t h;
@@ -207,7 +223,9 @@ struct DevBuf {
             vh.push_back(h);
             e = hipMemMap(va + off, sz, 0, h, 0);
             if (e) return e;
-            vmap_bytes = off + sz;
+            vmaps.emplace_back(off, sz);
+            g_vmm_mapped.fetch_add(1);
+            g_vmm_live_bytes.fetch_add((int64_t)sz);
         }
         hipMemAccessDesc acc = {};
         acc.location = prop.location;
@@ -219,18 +237,31 @@ struct DevBuf {
     }
     void release() {
         if (vres) {
-            if (vmap_bytes) {
-                const uintptr_t va = ((uintptr_t)vres + kVmmAlign - 1) / kVmmAlign * kVmmAlign;
-                hipMemUnmap(reinterpret_cast<void*>(va), vmap_bytes);
+            // each handle unmapped over exactly the range it was mapped at, every
+            // return code checked (a failure is counted and logged, and the rest still released)
+            char* va = vmm_base();
+            for (const auto& m : vmaps) {
+                const hipError_t e = hipMemUnmap(va + m.first, m.second);
+                if (e) {
+                    vmm_fail("hipMemUnmap", e);
+                } else {
+                    g_vmm_unmapped.fetch_add(1);
+                    g_vmm_live_bytes.fetch_sub((int64_t)m.second);
+                }
             }
-            for (auto h : vh) hipMemRelease(h);
-            hipMemAddressFree(vres, vres_bytes);
+            for (auto h : vh) {
+                const hipError_t e = hipMemRelease(h);
+                if (e) vmm_fail("hipMemRelease", e);
+            }
+            const hipError_t e = hipMemAddressFree(vres, vres_bytes);
+            if (e) vmm_fail("hipMemAddressFree", e);
         } else if (p) {
             hipFree(p);
         }
         vh.clear();
+        vmaps.clear();
         vres = nullptr;
-        vres_bytes = vmap_bytes = 0;
+        vres_bytes = 0;
         p = nullptr;
         bytes = 0;
     }
@@ -332,6 +363,8 @@ struct psgd_ctx {
     int64_t alpha_n = -1;
     double alpha_step = NAN, alpha_reg = NAN;
     bool alpha_ok = false;
+    // the fp64 CSR weight-vector size whose allocation failed (0: none): not retried
+    size_t wf64_failed = 0;
 };
 
 namespace {
@@ -1108,7 +1141,10 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         // kernels will run (chain_general keeps its weights in w_out, and C5's
         // vectors are ~34 GB); if HBM cannot hold them the epoch runs chain_general instead.
         const int64_t stride = 2 * (((int64_t)d + 128 + 1024 + 63) / 64 * 64);
-        if (ctx->wf32.ensure((size_t)P * (size_t)stride * sizeof(float), true) == hipSuccess) {
+        const size_t need = (size_t)P * (size_t)stride * sizeof(float);
+        // (a size that failed once is not retried every epoch -- each retry frees the
+        // old buffer and tries the VMM chunks and a hipMalloc of tens of GB again)
+        if (need != ctx->wf64_failed && ctx->wf32.ensure(need, true) == hipSuccess) {
             HIP_TRY(ctx->walpha.ensure((size_t)P * sizeof(double)));
             HIP_TRY(ctx->wnsq0.ensure(sizeof(double)));
             L.wstride = stride;
@@ -1117,6 +1153,10 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
             L.wnsq0 = ctx->wnsq0.as<double>();
         } else {
             (void)hipGetLastError();   // the failed allocation is not the epoch's error
+            if (need != ctx->wf64_failed)
+                fprintf(stderr, "psgd: the fp64 CSR chains' weight vectors (%zu bytes) do not fit in HBM: "
+                        "this epoch and later ones of this size run chain_general (variant 201)\n", need);
+            ctx->wf64_failed = need;
         }
     }
     if (params->gradient == PSGD_GRADIENT_LOGISTIC && params->compute_dtype == PSGD_F32 &&
@@ -1377,6 +1417,15 @@ int32_t psgd_ctx_last_chain_ms(psgd_ctx* ctx, double* ms_out) {
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, ctx->ev_begin, ctx->ev_end));
     *ms_out = ms;
+    return PSGD_OK;
+}
+
+int32_t psgd_vmm_stats(int64_t* out4) {
+    if (!out4) return fail(PSGD_EINVAL, "out4 is null");
+    out4[0] = g_vmm_mapped.load();
+    out4[1] = g_vmm_unmapped.load();
+    out4[2] = g_vmm_live_bytes.load();
+    out4[3] = g_vmm_failures.load();
     return PSGD_OK;
 }
 

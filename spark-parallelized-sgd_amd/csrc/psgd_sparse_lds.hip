@@ -582,6 +582,13 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
         // read in flight: with the tagger a few rows ahead, that happened every few samples)
         const unsigned ld_pre = TAIL ? __hip_atomic_load(&hdr->loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0u;
         const unsigned tg_pre = __hip_atomic_load(&hdr->tagged, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // the counts cached from these relaxed loads let the next samples' need()
+        // skip wait_for's fence and read the rows the loader / tagger published. That is sound
+        // because (1) LDS operations of a workgroup execute in order (the loader and the tagger
+        // write a row before its flag, this wave reads the flag before the row), and (2) no data
+        // load of a later sample may be hoisted by the compiler above these flag loads: the
+        // compiler-only fence below forbids it (no instruction, no lgkmcnt wait)
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
         __builtin_amdgcn_sched_barrier(0);
         T w0 = l0, w1 = l1;
         if constexpr (TAIL) {

@@ -244,6 +244,21 @@ class HipEngine(ShardedEngine):
     def gather_buffer(self):
         return self._gather
 
+    # (diagnostics) when a list, every cross-process exchange appends a pair of HIP events recorded
+    # around it on self.stream: the all-gather plus the rank-order fold (bench.py times them)
+    exchange_events = None
+
+    def exchange(self, partial):
+        if self.exchange_events is None:
+            return super().exchange(partial)
+        a = self.torch.cuda.Event(enable_timing=True)
+        b = self.torch.cuda.Event(enable_timing=True)
+        a.record(self.stream)
+        out = super().exchange(partial)
+        b.record(self.stream)
+        self.exchange_events.append((a, b))
+        return out
+
     def fold_partials(self, gathered):
         self.ctx.fold_partials_device(self.world, self.d, gathered.data_ptr(),
                                       self._folded.data_ptr(), self.stream.cuda_stream)

@@ -73,7 +73,8 @@ def _fake_record(spec, variant=302):
             "config": {"workload": f"{wl}: " + bench.WORKLOADS[wl][6] + " [this run: 20,000,000 rows]",
                        "rows_per_gpu": 20_000_000, "d": 4_194_304, "chains_per_gpu": 1024},
             "roofline": {"bound": "hbm", "achieved": 6543.21, "peak": 8000.0, "unit": "GB/s",
-                         "frac": 0.81790123, "traffic": 2.1e11, "traffic_source": "profiles/r04_c5_f64_pmc.json",
+                         "frac": 0.81790123, "frac_step": 0.79123456, "traffic": 2.1e11,
+                         "traffic_source": "profiles/r04_c5_f64_pmc.json",
                          "kernel": bench.kernel_name(variant), "bytes_per_launch": 4.8e10,
                          "bytes_per_sample": 2416, "avg_kernel_ms": 94.7169, "avg_epoch_ms": 100.36,
                          "variant": variant, "timing": "HIP events recorded around each chain-kernel launch"},
@@ -131,6 +132,35 @@ def test_final_line_multi_gpu():
     assert len(line) < bench.LINE_LIMIT
     got = json.loads(line)
     assert got["n_gpus"] == 8 and "secondary_summary" not in got
+
+
+def test_final_line_multi_gpu_with_baseline_secondaries():
+    """at N = 8 the line carries BASELINE's own 8-GPU configs as secondaries
+    (c3's 12.5M-row shard per GPU = configs[2], c5's 125M-row shard = configs[4]) with every
+    rank's chain-kernel ms and all-gather + fold ms, and stays one parseable line under the cap."""
+    import json
+    specs = bench.DEFAULT_SECONDARY_MULTI.split(",")
+    assert specs[0] == "c3:f32" and "c5:f32" in specs
+    assert bench.SECONDARY_ROWS_MULTI["c5"] == 125_000_000 and bench.WORKLOADS["c3"][1] == 12_500_000
+    ranks = {"kernel_ms": [7.7354 + i / 1000 for i in range(8)], "xchg_ms": [0.0412 + i / 1e4 for i in range(8)]}
+    records = []
+    for sp in specs:
+        r = _fake_record(sp, 304 if sp.startswith("c3") else 401)
+        r["ranks"] = ranks
+        if sp.startswith("c5"):
+            r["c5_store_probe"] = {"rows_per_chain": 2000, "ms": 8.5123, "ns_per_row": 4.156, "mode": "fast"}
+        records.append(r)
+    out = _headline(8)
+    out["ranks"] = ranks
+    line = bench.final_line(out, records)
+    assert len(line.encode()) < bench.LINE_LIMIT
+    got = json.loads(line)
+    assert got["n_gpus"] == 8 and len(got["ranks"]["kernel_ms"]) == 8
+    assert [e["spec"] for e in got["secondary_summary"]] == specs
+    for e in got["secondary_summary"]:
+        assert len(e["ranks"]["xchg_ms"]) == 8 and "frac_step" in e
+    assert got["secondary_summary"][-1]["c5_store_probe"]["mode"] == "fast"
+    assert "frac_step" in got["roofline"]
 
 
 def test_final_line_shrinks_when_too_long():

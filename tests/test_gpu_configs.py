@@ -404,7 +404,8 @@ def test_bench_two_ranks_gloo():
     the driver's 8-GPU node runs the nccl form). The line reports both ranks' samples."""
     import json
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
-           "--rows", "200000", "--secondary", "", "--steps", "3", "--warmup", "1", "--prewarm-s", "0.2"]
+           "--rows", "200000", "--secondary", "c3:f32", "--secondary-rows", "100000",
+           "--steps", "3", "--warmup", "1", "--prewarm-s", "0.2"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -415,3 +416,11 @@ def test_bench_two_ranks_gloo():
     assert out["value"] > 0 and out["prewarm"]["epochs"] >= 2
     # both ranks' rows were counted: value = 2 * 200,000 samples per step / the step time
     assert abs(out["value"] * out["ms_per_step"] / 1e3 - 400_000) < 1.0, out
+    # every rank's chain-kernel and all-gather + fold times, and the step-level roofline
+    assert len(out["ranks"]["kernel_ms"]) == 2 and len(out["ranks"]["xchg_ms"]) == 2, out["ranks"]
+    assert all(t > 0 for t in out["ranks"]["kernel_ms"] + out["ranks"]["xchg_ms"])
+    assert 0 < out["roofline"]["frac_step"] <= out["roofline"]["frac"] * 1.05
+    # the N > 1 secondary: BASELINE configs[2]'s per-GPU shard (c3), here at 100,000 rows per rank
+    sec = out["secondary_summary"]
+    assert [e["spec"] for e in sec] == ["c3:f32"] and "error" not in sec[0], sec
+    assert len(sec[0]["ranks"]["kernel_ms"]) == 2 and sec[0]["frac_step"] > 0
