@@ -690,6 +690,7 @@ def main():
         "dtype": res["dtype"], "data": "synthetic (device-generated, resident in HBM)",
         "config": res["config"], "roofline": res["roofline"], "prewarm": res["prewarm"],
         **({"ranks": res["ranks"]} if "ranks" in res else {}),
+        **({"c5_store_probe": res["c5_store_probe"]} if "c5_store_probe" in res else {}),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(grad, d, P, step, args.cpu_seconds,

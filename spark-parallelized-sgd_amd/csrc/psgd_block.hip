@@ -17,8 +17,8 @@
 //
 // so the only sequential work left per sample is scalar (c_i from z_i, one FMA per lane). The
 // rounding differs from the per-sample form (dot products reassociated, updates fused), which
-// is the fp32 throughput mode's stated tolerance; the fp64 parity mode keeps the
-// per-sample kernels of psgd_kernels.hip.
+// is the fp32 throughput mode's stated tolerance; the fp64 parity mode runs the
+// same blocked recurrence in doubles (chain_block64, psgd_block64.hip).
 //
 // One workgroup = one chain = four waves, one per SIMD:
 //   wave 0 (chain)   owns W in VGPRs (lane l: features (v*64+l)*VEC ..), per block: reads the K

@@ -226,6 +226,11 @@ static_assert(kFixed64 % 16 == 0, "the meta and row rings start 16-byte aligned"
 #ifndef PSGD_B64_INTERLEAVE
 #define PSGD_B64_INTERLEAVE 1
 #endif
+// cost probes (tools/chain_bench64 builds only; wrong results): 1 the recurrence without its
+// dependency (z not moved by the Gram terms), 2 no wait for the other chain wave's partials
+#ifndef PSGD_B64_EXP
+#define PSGD_B64_EXP 0
+#endif
 
 // doubles per Gram ring slot: the 8x8 triangle, and with the per-sample break the block's 8
 // squared row norms
@@ -706,7 +711,9 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
             q = gring[gs * GSL + kB * kB + krow];
             if constexpr (FS) q += gring[gs * GSL + GSZ + kB * kB + krow];
         }
-        if constexpr (H == 2) {
+        if constexpr (H == 2 && (PSGD_B64_EXP & 2)) {
+            z = z + z;
+        } else if constexpr (H == 2) {
             // the other chain wave's partial of this lane's row: z = p0 + p1 in both waves
             const unsigned need = (unsigned)(b + 1);
             unsigned* xo = &xhdr->xdone[h ^ 1];
@@ -775,6 +782,8 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
             if constexpr (UPD == U_SQUARED_L2) {
                 if (krow == i) zf = z;
                 if (i + 1 < kB) z = __builtin_fma(c[i], G[i], al[i] * z);
+            } else if constexpr (PSGD_B64_EXP & 1) {
+                if (i + 1 < kB) zf = __builtin_fma(c[i], G[i], zf);
             } else {
                 if (i + 1 < kB) z = __builtin_fma(c[i], G[i], z);
             }
@@ -784,7 +793,7 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
             // r05: c3 Logistic f32 rows 488 -> 492 cycles per row, c2 LeastSquares 239 -> 242)
             if constexpr (PSGD_B64_INTERLEAVE) update_row(i);
         }
-        if constexpr (UPD != U_SQUARED_L2) zf = z;
+        if constexpr (UPD != U_SQUARED_L2 && !(PSGD_B64_EXP & 1)) zf = z;
         // (a lane's z stops moving after its row's step: G[k][i] = 0 for i >= k; SquaredL2's zf
         // keeps it through the later rows' shrinks)
         if constexpr (CONV && GRAD != G_LOGISTIC) ck = coef64<GRAD>(zf, yv, nsv);

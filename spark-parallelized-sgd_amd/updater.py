@@ -40,7 +40,8 @@ class L1SGDUpdater(SGDUpdater):
 
 class AdaGradSGDUpdater(SGDUpdater):
     """accum += g*g; w' = w - s * g / sqrt(accum + 1.0) (SGDUpdater.scala:193-228).
-    Per-chain status (accum) lives in HBM; dense and CSR rows."""
+    Per-chain status (accum): in the chain's registers on dense rows (chain_split / chain_dense),
+    in HBM on CSR rows and past the register-resident width (chain_general); dense and CSR rows."""
 
     kind = 3
 

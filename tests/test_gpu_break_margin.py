@@ -69,11 +69,27 @@ CASES = {
     "general_csr": ("csr", 3000, np.float32, "f64", "simple", 0.0, 1.0, {"PSGD_PER_SAMPLE": "1"}, None),
     "block_f32": ("dense", 700, np.float32, "f32", "simple", 0.0, 4.0 / 700, {}, None),
     "sparse_lds_f32": ("csr", 3000, np.float32, "f32", "simple", 0.0, 1.0, {}, None),
+
+
+    "block_f32_l2": ("dense", 700, np.float32, "f32", "squared_l2", 0.05, 4.0 / 700, {}, None),
 }
+# the same probes with the break inside a TAIL block (a chain length that is not a
+# multiple of the 8-row block, the flip sample in its last, partial block): chain_block64's kpair
+# butterfly and chain_block's bpermute scan are separate instantiations there
+TAIL_CASES = ("block64_h1_simple", "block64_h2_simple", "block64_h2_l2", "block_f32", "block_f32_l2")
 
 
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_adversarial_break(pkg, oracle, monkeypatch, name):
+    run_case(pkg, oracle, monkeypatch, name, tail=False)
+
+
+@pytest.mark.parametrize("name", TAIL_CASES)
+def test_adversarial_break_in_tail_block(pkg, oracle, monkeypatch, name):
+    run_case(pkg, oracle, monkeypatch, name, tail=True)
+
+
+def run_case(pkg, oracle, monkeypatch, name, tail):
     layout, d, dtype, compute, upd, reg, step, env, want_variant = CASES[name]
     for k in ("PSGD_B64_CONV", "PSGD_PER_SAMPLE", "PSGD_SPARSE_KERNEL", "PSGD_SPARSE_SK", "PSGD_SPARSE_LDS_HEAD"):
         monkeypatch.delenv(k, raising=False)
@@ -83,22 +99,38 @@ def test_adversarial_break(pkg, oracle, monkeypatch, name):
     P, rows = 8, 160
     n = P * rows
     offs = [i * rows for i in range(P + 1)]
+    chain = 3
     if layout == "dense":
         X, y = synth(rng, n, d, "logistic", dtype)
-        data = pkg.PartitionedData.parallelize(y, X, P, dtype=dtype)
         mat = oracle.Matrix(y, X.astype(np.float64))
     else:
         rp, col, val, y = synth_csr(rng, n, d, 5, 40)
         vs = val.astype(dtype)
-        data = pkg.PartitionedData([pkg.CsrPartition(y[a:b], rp[a:b + 1] - rp[a], col[rp[a]:rp[b]],
-                                                     vs[rp[a]:rp[b]], d) for a, b in zip(offs[:-1], offs[1:])])
         mat = oracle.Matrix(y, row_ptr=rp, col=col, val=vs.astype(np.float64), d=d)
-    chain = 3
     r = oracle.ratio_trace(mat, offs, chain, "logistic", upd, step, reg, np.zeros(d))
     assert len(r) == rows
     # a record low in the chain's middle, clear of every earlier sample by far more than 1e-5
-    k = next(k for k in range(rows // 3, rows) if r[k] < r[:k].min() * (1 - 1e-4))
-    rec = {"sample": int(k), "r_k": float(r[k]), "variant": None, "decisions": {}}
+    lows = [k for k in range(rows // 3, rows) if r[k] < r[:k].min() * (1 - 1e-4)]
+    if tail:
+        # truncate the chain to 8 (k // 8) + 7 rows: sample k then sits in the partial last block
+        # (the rows of the chain before it are unchanged, so is its trace)
+        lows = [k for k in lows if k % 8 != 7]
+    k = lows[0]
+    if tail:
+        keep = offs[chain] + 8 * (k // 8) + 7
+        drop = np.arange(keep, offs[chain + 1])
+        y = np.delete(y, drop)
+        X = np.delete(X, drop, axis=0)
+        offs = offs[:chain + 1] + [o - len(drop) for o in offs[chain + 1:]]
+        mat = oracle.Matrix(y, X.astype(np.float64))
+        assert (offs[chain + 1] - offs[chain]) % 8 == 7
+    if layout == "dense":
+        data = pkg.PartitionedData([pkg.DensePartition(y[a:b], X[a:b]) for a, b in zip(offs[:-1], offs[1:])])
+    else:
+        data = pkg.PartitionedData([pkg.CsrPartition(y[a:b], rp[a:b + 1] - rp[a], col[rp[a]:rp[b]],
+                                                     vs[rp[a]:rp[b]], d) for a, b in zip(offs[:-1], offs[1:])])
+    rec = {"sample": int(k), "r_k": float(r[k]), "variant": None, "decisions": {},
+           "chain_rows": int(offs[chain + 1] - offs[chain])}
     for e in EPS:
         for sgn in (1, -1):
             tol = float(r[k] * (1 + sgn * e))
@@ -117,9 +149,11 @@ def test_adversarial_break(pkg, oracle, monkeypatch, name):
     if want_variant is not None:
         assert rec["variant"] == want_variant, (name, rec["variant"])
     # below the bound (and in fp32) the kernel may decide either way, but only between the two
-    # reference outcomes: break at k, or carry on to the reference's next break
+    # reference outcomes: break at k, or carry on to the reference's next break (in a truncated
+    # chain: its end)
     plus, minus = rec["decisions"]["+1e-15"]["ref"], rec["decisions"]["-1e-15"]["ref"]
     for v in rec["decisions"].values():
         assert v["kernel"] in (plus, minus) or compute == "f32", (name, v)
-    RESULTS[name] = rec
-    print(name, rec["variant"], {e: (v["kernel"], v["ref"]) for e, v in rec["decisions"].items()})
+    key = name + ("@tail" if tail else "")
+    RESULTS[key] = rec
+    print(key, rec["variant"], {e: (v["kernel"], v["ref"]) for e, v in rec["decisions"].items()})
