@@ -72,11 +72,16 @@ CASES = {
 
 
     "block_f32_l2": ("dense", 700, np.float32, "f32", "squared_l2", 0.05, 4.0 / 700, {}, None),
+    # LeastSquares + Simple: chain_block64's block solve (round 6) decides these
+    "block64_h1_ls": ("dense", 60, np.float64, "f64", "simple", 0.0, 0.002, {}, 741),
+    "block64_h2_ls": ("dense", 700, np.float32, "f64", "simple", 0.0, 0.002, {}, 754),
 }
+GRADIENT = {"block64_h1_ls": "least_squares", "block64_h2_ls": "least_squares"}   # else logistic
 # the same probes with the break inside a TAIL block (a chain length that is not a
 # multiple of the 8-row block, the flip sample in its last, partial block): chain_block64's kpair
 # butterfly and chain_block's bpermute scan are separate instantiations there
-TAIL_CASES = ("block64_h1_simple", "block64_h2_simple", "block64_h2_l2", "block_f32", "block_f32_l2")
+TAIL_CASES = ("block64_h1_simple", "block64_h2_simple", "block64_h2_l2", "block_f32", "block_f32_l2",
+              "block64_h2_ls")
 
 
 @pytest.mark.parametrize("name", sorted(CASES))
@@ -91,6 +96,7 @@ def test_adversarial_break_in_tail_block(pkg, oracle, monkeypatch, name):
 
 def run_case(pkg, oracle, monkeypatch, name, tail):
     layout, d, dtype, compute, upd, reg, step, env, want_variant = CASES[name]
+    grad = GRADIENT.get(name, "logistic")
     for k in ("PSGD_B64_CONV", "PSGD_PER_SAMPLE", "PSGD_SPARSE_KERNEL", "PSGD_SPARSE_SK", "PSGD_SPARSE_LDS_HEAD"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
@@ -101,13 +107,13 @@ def run_case(pkg, oracle, monkeypatch, name, tail):
     offs = [i * rows for i in range(P + 1)]
     chain = 3
     if layout == "dense":
-        X, y = synth(rng, n, d, "logistic", dtype)
+        X, y = synth(rng, n, d, grad, dtype)
         mat = oracle.Matrix(y, X.astype(np.float64))
     else:
         rp, col, val, y = synth_csr(rng, n, d, 5, 40)
         vs = val.astype(dtype)
         mat = oracle.Matrix(y, row_ptr=rp, col=col, val=vs.astype(np.float64), d=d)
-    r = oracle.ratio_trace(mat, offs, chain, "logistic", upd, step, reg, np.zeros(d))
+    r = oracle.ratio_trace(mat, offs, chain, grad, upd, step, reg, np.zeros(d))
     assert len(r) == rows
     # a record low in the chain's middle, clear of every earlier sample by far more than 1e-5
     lows = [k for k in range(rows // 3, rows) if r[k] < r[:k].min() * (1 - 1e-4)]
@@ -134,9 +140,9 @@ def run_case(pkg, oracle, monkeypatch, name, tail):
     for e in EPS:
         for sgn in (1, -1):
             tol = float(r[k] * (1 + sgn * e))
-            _, _, ref = oracle.run(mat, offs, "logistic", upd, step, 1, reg, np.zeros(d), tol=tol,
+            _, _, ref = oracle.run(mat, offs, grad, upd, step, 1, reg, np.zeros(d), tol=tol,
                                    margin_check=False)
-            _, _, got = pkg.runParallelizedSGD(data, pkg.LogisticGradient(), getattr(pkg, U[upd])(), step, 1,
+            _, _, got = pkg.runParallelizedSGD(data, getattr(pkg, G[grad])(), getattr(pkg, U[upd])(), step, 1,
                                                reg, 1.0, np.zeros(d), tol, compute_dtype=compute,
                                                return_chain_counts=True)
             rec["variant"] = pkg.optimization.get_context(0).last_kernel()
