@@ -148,7 +148,8 @@ def test_final_line_multi_gpu_with_baseline_secondaries():
         r = _fake_record(sp, 304 if sp.startswith("c3") else 401)
         r["ranks"] = ranks
         if sp.startswith("c5"):
-            r["c5_store_probe"] = {"rows_per_chain": 2000, "ms": 8.5123, "ns_per_row": 4.156, "mode": "fast"}
+            r["c5_store_probe"] = {"rows_per_chain": 2000, "probe_ms": 12.7094, "marginal_ns_per_row": 3.912,
+                                   "mode": "fast"}
         records.append(r)
     out = _headline(8)
     out["ranks"] = ranks

@@ -85,9 +85,10 @@ def test_vmm_chunks_released_on_regrow_and_destroy(pkg, monkeypatch):
     # the regrow released the first set chunk by chunk and mapped a larger one
     assert s2["unmapped"] - s1["unmapped"] == s1["mapped"] - s0["mapped"]
     assert s2["mapped"] - s1["mapped"] > s1["mapped"] - s0["mapped"]
-    assert s3["mapped"] > s2["mapped"] and s3["live_bytes"] >= 16 * d * 8
+    mine = s3["live_bytes"] - s0["live_bytes"]   # (the counters are process-wide: other contexts' too)
+    assert s3["mapped"] > s2["mapped"] and mine >= 16 * d * 8
     # while mapped, the chunks are visible in the device's free memory ...
-    assert free[3] <= free0 - s3["live_bytes"] + (8 << 20), (free0, free[3], s3)
+    assert free[3] <= free0 - mine + (8 << 20), (free0, free[3], s0, s3)
     # ... and after psgd_ctx_destroy every chunk is unmapped and released, none failed
     assert s4["failures"] == s0["failures"], s4
     assert s4["mapped"] - s0["mapped"] == s4["unmapped"] - s0["unmapped"], s4
