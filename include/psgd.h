@@ -192,6 +192,11 @@ int32_t psgd_ctx_last_chain_ms(psgd_ctx* ctx, double* ms_out);
  * unmapped, [2] bytes currently mapped, [3] failed unmap / release / address-free calls. */
 int32_t psgd_vmm_stats(int64_t* out4);
 
+/* Diagnostics (no reference counterpart): process-wide counters of the placement re-roll of the
+ * CSR chains' weight-vector sets below the VMM threshold (PSGD_REROLL candidates):
+ * out2[0] sets probed, [1] sets where a later candidate was kept. */
+int32_t psgd_reroll_stats(int64_t* out2);
+
 /* The device sampler of one partition, alone: RDD.sample(false, fraction, .) over a partition
  * of n rows whose PartitionwiseSampledRDD seed is `seed` (the partition's java.util.Random
  * nextLong, before hashSeed) [ext Spark 1.6.1 BernoulliSampler] -- the batch selection

@@ -24,7 +24,7 @@ EXPORTED = (
     "psgd_register_dense", "psgd_register_csr", "psgd_register_dense_device", "psgd_register_csr_device",
     "psgd_clear_partitions", "psgd_num_partitions", "psgd_run_epoch", "psgd_run_epoch_device",
     "psgd_fold_partials_device", "psgd_convergence_terms_device", "psgd_initial_regval",
-    "psgd_ctx_last_kernel", "psgd_ctx_last_chain_ms", "psgd_vmm_stats", "psgd_libsvm_read", "psgd_libsvm_free",
+    "psgd_ctx_last_kernel", "psgd_ctx_last_chain_ms", "psgd_vmm_stats", "psgd_reroll_stats", "psgd_libsvm_read", "psgd_libsvm_free",
     "psgd_sample_partition", "psgd_host_alloc", "psgd_host_free", "psgd_register_wait",
 )
 
@@ -104,6 +104,7 @@ def lib():
             "psgd_ctx_last_kernel": ([vp], C.c_int32),
             "psgd_ctx_last_chain_ms": ([vp, dp], C.c_int32),
             "psgd_vmm_stats": ([i64p], C.c_int32),
+            "psgd_reroll_stats": ([i64p], C.c_int32),
             "psgd_libsvm_read": ([C.c_char_p, C.c_int32, C.c_int32, C.POINTER(C.POINTER(psgd_libsvm))], C.c_int32),
             "psgd_libsvm_free": ([C.POINTER(psgd_libsvm)], None),
             "psgd_sample_partition": ([C.c_int32, C.c_int64, C.c_int64, C.c_double, vp, i64p], C.c_int32),
@@ -135,6 +136,13 @@ def vmm_stats() -> dict:
     out = (C.c_int64 * 4)()
     check(lib().psgd_vmm_stats(out))
     return {"mapped": out[0], "unmapped": out[1], "live_bytes": out[2], "failures": out[3]}
+
+
+def reroll_stats() -> dict:
+    """Process-wide counters of the CSR vector sets' placement re-roll (psgd_reroll_stats)."""
+    out = (C.c_int64 * 2)()
+    check(lib().psgd_reroll_stats(out))
+    return {"sets": out[0], "swaps": out[1]}
 
 
 def sample_partition(seed: int, n: int, fraction: float, device: int = 0):

@@ -162,6 +162,7 @@ static void vmm_fail(const char* what, hipError_t e) {
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    bool fresh = false;   // allocated by the last ensure() (reroll_vectors consumes it)
     // a virtual-memory mapping (vmm_map): the reservation, the physical handles and, per handle,
     // the (offset, size) it is mapped at inside the aligned range -- unmapped one by one, as mapped
     void* vres = nullptr;
@@ -186,7 +187,10 @@ struct DevBuf {
             }
         }
         if (e != hipSuccess && !p) e = hipMalloc(&p, need);
-        if (e == hipSuccess) bytes = need;
+        if (e == hipSuccess) {
+            bytes = need;
+            fresh = true;
+        }
         return e;
     }
     char* vmm_base() const {
@@ -268,6 +272,75 @@ struct DevBuf {
     template <typename T>
     T* as() const { return static_cast<T*>(p); }
 };
+
+// PSGD_REROLL (default 8): how many allocations a CSR vector set below the VMM threshold is chosen
+// from (<= 1: the first). Measured round 6: the rate of the chains' scattered
+// read-modify-writes over their vectors is a property of the allocation (c4: 27.4 or 31.3 ms for
+// the same rows, by context), and a short probe of the same access pattern tells the two kinds
+// apart; the context probes a few candidates once, when it allocates the set, and keeps the fastest.
+static int reroll_candidates() {
+    const char* e = getenv("PSGD_REROLL");
+    const int k = e && *e ? atoi(e) : 8;
+    return k < 1 ? 1 : (k > 16 ? 16 : k);
+}
+static std::atomic<int64_t> g_reroll_sets{0}, g_reroll_swaps{0};
+
+// b holds n_vectors vectors of d_words used 4-byte words, stride_words apart. Replaces a freshly
+// hipMalloc'd b by the fastest of reroll_candidates() allocations of its size under the probe of
+// words [lo_words, d_words) of every vector -- the part past the LDS head, where the chains'
+// scattered accesses go (probing the whole vector separated the two kinds of allocation by ~2.5 %,
+// the tail alone by ~20 %: tools/place_probe.hip, profiles/r06_c4_placement.log).
+static void reroll_vectors(DevBuf& b, int64_t stride_words, int n_vectors, int d_words, int lo_words,
+                           hipStream_t st) {
+    if (!b.fresh) return;
+    b.fresh = false;
+    const int K = reroll_candidates();
+    if (K <= 1 || b.vres || !b.p || b.bytes >= vmm_min() || n_vectors <= 0) return;
+    if (lo_words < 0 || lo_words >= d_words) lo_words = 0;
+    std::vector<void*> cand{b.p};
+    for (int k = 1; k < K; ++k) {
+        void* q = nullptr;
+        if (hipMalloc(&q, b.bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            break;
+        }
+        cand.push_back(q);
+    }
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    size_t best = 0;
+    float best_ms = 0.0f;
+    std::vector<float> ms(cand.size(), -1.0f);
+    if (hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess) {
+        for (size_t i = 0; i < cand.size(); ++i) {
+            float* w = static_cast<float*>(cand[i]) + lo_words;
+            const int span = d_words - lo_words;
+            if (psgd::launch_vector_probe(w, stride_words, n_vectors, span, 256, 11u, st)) break;
+            (void)hipEventRecord(e0, st);
+            if (psgd::launch_vector_probe(w, stride_words, n_vectors, span, 2000, 12345u, st)) break;
+            (void)hipEventRecord(e1, st);
+            if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms[i], e0, e1) != hipSuccess) break;
+            if (i == 0 || ms[i] < best_ms) {
+                best = i;
+                best_ms = ms[i];
+            }
+        }
+    }
+    (void)hipGetLastError();
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    (void)hipStreamSynchronize(st);   // no probe still runs on a candidate that is freed below
+    for (size_t i = 0; i < cand.size(); ++i)
+        if (i != best) (void)hipFree(cand[i]);
+    b.p = cand[best];
+    g_reroll_sets.fetch_add(1);
+    if (best != 0) g_reroll_swaps.fetch_add(1);
+    const char* lg = getenv("PSGD_REROLL_LOG");
+    if (lg && lg[0] == '1') {
+        fprintf(stderr, "psgd: vector set of %zu bytes, probe ms:", b.bytes);
+        for (float m : ms) fprintf(stderr, " %.3f", m);
+        fprintf(stderr, " -> kept %zu\n", best);
+    }
+}
 
 // Pinned staging ring of the host -> HBM ingest (registration from pageable host memory):
 // kStageSlots pinned buffers; the host packs chunk k + 1 into one while chunk k's DMA runs from
@@ -1124,6 +1197,8 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         // (rows 256-byte aligned: the epoch's init kernel stores 16-byte vectors)
         L.wstride = ((int64_t)d + 128 + 1024 + 63) / 64 * 64;
         HIP_TRY(ctx->wf32.ensure((size_t)P * (size_t)L.wstride * sizeof(float), true));
+        // (the fp32 LDS head of chain_sparse_lds; below it the chains never touch the vector)
+        reroll_vectors(ctx->wf32, L.wstride, P, d, (int)std::max<int64_t>(psgd::sparse_lds_head(d), 0), st);
         HIP_TRY(ctx->walpha.ensure((size_t)P * sizeof(double)));
         HIP_TRY(ctx->wnsq0.ensure(sizeof(double)));
         L.wf32 = ctx->wf32.as<float>();
@@ -1145,6 +1220,8 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         // (a size that failed once is not retried every epoch -- each retry frees the
         // old buffer and tries the VMM chunks and a hipMalloc of tens of GB again)
         if (need != ctx->wf64_failed && ctx->wf32.ensure(need, true) == hipSuccess) {
+            // (the fp64 head is shorter than the fp32 one: half of it is inside the fp64 tail)
+            reroll_vectors(ctx->wf32, stride, P, 2 * d, (int)std::max<int64_t>(psgd::sparse_lds_head(d), 0), st);
             HIP_TRY(ctx->walpha.ensure((size_t)P * sizeof(double)));
             HIP_TRY(ctx->wnsq0.ensure(sizeof(double)));
             L.wstride = stride;
@@ -1426,6 +1503,13 @@ int32_t psgd_vmm_stats(int64_t* out4) {
     out4[1] = g_vmm_unmapped.load();
     out4[2] = g_vmm_live_bytes.load();
     out4[3] = g_vmm_failures.load();
+    return PSGD_OK;
+}
+
+int32_t psgd_reroll_stats(int64_t* out2) {
+    if (!out2) return fail(PSGD_EINVAL, "out2 is null");
+    out2[0] = g_reroll_sets.load();
+    out2[1] = g_reroll_swaps.load();
     return PSGD_OK;
 }
 

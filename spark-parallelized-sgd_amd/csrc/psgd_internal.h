@@ -147,6 +147,10 @@ bool sparse_lds64_applies(int64_t d, int64_t max_nnz, int updater, bool check_co
 int launch_sparse_lds64_chains(const ChainLaunch& L, const KParams& kp, int storage, int gradient,
                                int updater, int64_t max_nnz, hipStream_t stream, int* kernel_variant);
 // Longest row of a device-resident CSR partition (synchronises `st`).
+// Placement probe of the CSR chains' weight vectors (psgd_probe.hip): n_vectors waves, each
+// `iters` random 4-byte read-modify-writes per lane over its vector's first d_words words.
+int launch_vector_probe(float* w, int64_t stride_words, int n_vectors, int d_words, int iters, unsigned seed,
+                        hipStream_t st);
 int csr_max_nnz(const int64_t* d_row_ptr, int64_t n, int64_t* out, hipStream_t st);
 // RDD.sample(false, fraction, seed) per partition (PSGD.scala:242): from the registered
 // descriptors `base`, the epoch's descriptors `out` (rows/y/n_rows of the sampled subsequence;
