@@ -235,9 +235,19 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
     // in wave order. A stopped chain leaves collect with whatever it read (the host raises on the
     // watchdog word).
     constexpr uint64_t kMask = XW == 64 ? ~0ull : ((1ull << XW) - 1);
+    // H = 1 (the diagnostic PSGD_SPLIT_HMAX=1 builds only: the product runs H = min(NV, 4) >= 2 --
+    // one-vector rows take chain_dense): one wave holds every partial, so there is no exchange;
+    // publish keeps the values and collect returns them (round 6: the per-H table's H = 1 row
+    // without the wave's LDS round trip to itself)
+    T xown[KV];
     // Every lane writes (no EXEC juggling on the per-sample path): lanes past the wave's PC * KV
     // words write its last word again, with the same value (the partials are wave-uniform).
     auto publish = [&](const T (&val)[KV], int32_t t) __attribute__((always_inline)) {
+        if constexpr (H == 1) {
+#pragma unroll
+            for (int q = 0; q < KV; ++q) xown[q] = val[q];
+            return;
+        }
         const int l = lane < PC * KV ? lane : PC * KV - 1;
         const int k = l / PC;
         T vk = val[0];
@@ -258,6 +268,11 @@ __global__ __launch_bounds__(64 * (H + 1)) void chain_split(ChainLaunch L, KPara
     // bits) -- no readlane and no SGPR round trip on the sample's path.
     constexpr bool kLaneSum = KV == 1 && (H == 2 || H == 4);
     auto collect = [&](int32_t t, T (&sum)[KV]) __attribute__((always_inline)) {
+        if constexpr (H == 1) {
+#pragma unroll
+            for (int q = 0; q < KV; ++q) sum[q] = xown[q];
+            return;
+        }
         const uint32_t tag = (uint32_t)(t + 1);
         const uint64_t* src = xw + (int)(t & 1) * XW + (kLaneSum ? PC * (lane & (H - 1)) : (lane < XW ? lane : 0));
         constexpr uint64_t kNeed = kLaneSum ? ~0ull : kMask;
