@@ -1,12 +1,12 @@
 #!/bin/bash
 # chain_split per-sample cycle split at c3 for H = 1, 2, 4 compute waves:
 # the diagnostic builds `make -C spark-parallelized-sgd_amd/csrc stamps_h` (PSGD_SPLIT_HMAX=1/2,
-# and 4 = tools/libpsgd_stamps.so), one bench epoch each with PSGD_STAMPS=1 (stderr: per compute
+# and 4: stamps_h4 -- round 6; round 5 used tools/libpsgd_stamps.so), one bench epoch each with PSGD_STAMPS=1 (stderr: per compute
 # wave, cycles per sample: total, dot + reduction, exchange wait, multiplier + update).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 out=gpurun_out/split_h
 mkdir -p $out
-for lib in stamps_h1 stamps_h2 stamps; do
+for lib in ${LIBS:-stamps_h1 stamps_h2 stamps_h4}; do
   for spec in "f32 adagrad" "f32 adam" "f64 adagrad" "f64 adam"; do
     set -- $spec
     f=$out/${lib}_$1_$2.log
