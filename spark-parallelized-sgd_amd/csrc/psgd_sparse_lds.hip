@@ -63,7 +63,7 @@ constexpr int LCAP = 128;                  // entries per row (two per lane)
 #define PSGD_LDS_NT 1                      // the loader's CSR entry loads are non-temporal
 #endif
 #ifndef PSGD_LDS_EXP
-#define PSGD_LDS_EXP 0                     // cost probes (tools/r03_c4_probe.sh); 0 in the product
+#define PSGD_LDS_EXP 0                     // cost probes (tools/r03_c4_probe.sh, tools/r06_c4_probe.sh); 0 in the product
 #endif
 
 // The chain's tail gathers and stores are buffer instructions over its fp32 vector: a 32-bit
@@ -597,17 +597,26 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
             // compiled out of the product: an s_memtime on any path into the arithmetic below
             // makes the compiler wait for every LDS read in flight, the next row's prefetch too)
             PSGD_STAMP(uint64_t vm0 = 0; if (L.stamps) vm0 = __builtin_amdgcn_s_memtime();)
+#if PSGD_LDS_EXP & 16   // experiment: no wait for the row's gathers, their values unused (cost probe)
+            w0 = l0;
+            w1 = l1;
+#else
             asm volatile("s_waitcnt vmcnt(%2)" : "+v"(gr[Q][0]), "+v"(gr[Q][1]) : "i"(4 * SK) : "memory");
             PSGD_STAMP(if (L.stamps) st_wait += __builtin_amdgcn_s_memtime() - vm0;)
             // head: W[j]; tail also in rows t-SK .. t-1: that row's new value; else the gather
             w0 = r0 == kLdsDummy ? gr[Q][0] : l0;
             w1 = r1 == kLdsDummy ? gr[Q][1] : l1;
+#endif
         }
         w0 = lane < cur.nnz ? w0 : T(0);
         w1 = lane + 64 < cur.nnz ? w1 : T(0);
         T acc = cur.x0 * w0;
         acc = m_fma(cur.x1, w1, acc);
+#if PSGD_LDS_EXP & 4    // experiment: no wave reduction, the lane's partial as the dot (cost probe)
+        T z = acc;
+#else
         T z = wave_sum_uniform(acc);
+#endif
         T qx = T(0);   // CONV: x . x
         if constexpr (CONV) qx = wave_sum_uniform(m_fma(cur.x1, cur.x1, cur.x0 * cur.x0));
         // CONV: a sample after the break is not taken (c = 0, no shrink, no loss)
@@ -627,7 +636,12 @@ __global__ __launch_bounds__(192) void chain_sparse_lds(ChainLaunch L, KParams k
             loss_sum += t < n && live ? loss : 0.0;
         } else {
             float loss;
+#if PSGD_LDS_EXP & 8    // experiment: the coefficient does not wait for the dot (cost probe)
+            asm volatile("" : : "v"(z));
+            c = sparse_coef<GRAD>(T(0.25) * cur.y, cur.y, cur.s, loss);
+#else
             c = sparse_coef<GRAD>(z, cur.y, cur.s, loss);
+#endif
             loss_blk += t < n && live ? loss : 0.0f;
             if ((t & 31) == 31) { loss_sum += double(loss_blk); loss_blk = 0.0f; }
         }
