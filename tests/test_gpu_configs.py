@@ -404,7 +404,7 @@ def test_bench_two_ranks_gloo():
     the driver's 8-GPU node runs the nccl form). The line reports both ranks' samples."""
     import json
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
-           "--rows", "200000", "--secondary", "c3:f32", "--secondary-rows", "100000",
+           "--rows", "200000", "--secondary", "c3:f32,c5:f32", "--secondary-rows", "100000",
            "--steps", "3", "--warmup", "1", "--prewarm-s", "0.2"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
@@ -422,5 +422,7 @@ def test_bench_two_ranks_gloo():
     assert 0 < out["roofline"]["frac_step"] <= out["roofline"]["frac"] * 1.05
     # the N > 1 secondary: BASELINE configs[2]'s per-GPU shard (c3), here at 100,000 rows per rank
     sec = out["secondary_summary"]
-    assert [e["spec"] for e in sec] == ["c3:f32"] and "error" not in sec[0], sec
+    assert [e["spec"] for e in sec] == ["c3:f32", "c5:f32"] and all("error" not in e for e in sec), sec
     assert len(sec[0]["ranks"]["kernel_ms"]) == 2 and sec[0]["frac_step"] > 0
+    # c5 (configs[4]'s shard, here 100,000 rows per rank) with its store-mode probe on each rank
+    assert len(sec[1]["ranks"]["xchg_ms"]) == 2 and "c5_store_probe" in sec[1], sec[1]
