@@ -18,6 +18,7 @@ import json
 import os
 import sys
 import time
+from collections import deque
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -443,19 +444,51 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
     w = engine.weights(np.zeros(d))
     stream = engine.stream  # the engine's kernels and copies all run on this stream
 
-    def one_step(w, it, ev=None):
-        params.iteration = it
-        if ev is not None:
-            ev[0].record(stream)
-        folded, _ = engine.epoch(params, w)
-        if ev is not None:
-            ev[1].record(stream)
-        rv, loss, cnt = engine.scalars(folded)  # D2H of the 3 driver scalars (PSGD:278-287)
-        if ev is not None:
-            kernel_ms.append(engine.ctx.last_chain_ms())  # HIP events around the chain launch
-        return (engine.adopt(folded) if cnt > 0 else w), cnt, loss
+    # tol == 0 with full batches: the driver's pipelined loop (ParallelizedSGD._run_pipelined --
+    # every epoch enqueued with the previous epoch's folded weights, its three scalars read back
+    # PIPELINE_LAG epochs later); otherwise the loop's synchronous form (scalars after each epoch)
+    pipelined = fraction >= 1.0 and tol == 0.0
+    lag = pkg.ParallelizedSGD.PIPELINE_LAG if pipelined else 0
 
-    kernel_ms = []
+    def run_epochs(w, it0, k, events=None):
+        """k epochs from iteration it0; events: k + 1 HIP events, one recorded on the engine
+        stream before each epoch and one after the last. Returns (w, last count, last loss,
+        total count)."""
+        pending = deque()
+        last = [0, 0.0, 0]
+
+        def settle(scalars):
+            _, loss, cnt = scalars   # the 3 driver scalars (PSGD:278-287)
+            last[0], last[1] = cnt, loss
+            last[2] += cnt
+            return cnt
+
+        for j in range(k):
+            params.iteration = it0 + j
+            if events is not None:
+                events[j].record(stream)
+            if pipelined:
+                folded, token = engine.epoch_async(params, w)
+            else:
+                folded, _ = engine.epoch(params, w)
+            if pipelined:
+                pending.append(token)
+                w = engine.adopt_view(folded)
+                if len(pending) > lag:
+                    settle(engine.scalars_wait(pending.popleft()))
+            elif settle(engine.scalars(folded)) > 0:
+                w = engine.adopt(folded)
+        if events is not None:
+            events[k].record(stream)
+        while pending:
+            settle(engine.scalars_wait(pending.popleft()))
+        return w, last[0], last[1], last[2]
+
+    def chain_ms_since(first):
+        """Device ms of the chain launches from launch `first` on (HIP events around each chain
+        launch on the engine stream; the context keeps the last 64)."""
+        end = engine.ctx.chain_launches()
+        return [engine.ctx.chain_ms(k) for k in range(max(first, end - 64), end)]
 
     # Device prewarm (part of setup, like data generation): the chain kernel's first launches run
     # below steady-state clocks (rocprof trace: 3.5-3.8 ms for the first c2 epochs, 3.1 ms from
@@ -469,9 +502,8 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
         wp = w0
         torch.cuda.synchronize()
         t_pw = time.perf_counter()
-        for _ in range(2):
-            wp, _, _ = one_step(wp, prewarm_epochs + 1)
-            prewarm_epochs += 1
+        wp, _, _, _ = run_epochs(wp, 1, 2)
+        prewarm_epochs = 2
         torch.cuda.synchronize()
         per_epoch = (time.perf_counter() - t_pw) / 2
         want = max(2, min(5000, int(prewarm_s / max(per_epoch, 1e-6))))
@@ -479,27 +511,25 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
             t = torch.tensor([want], dtype=torch.int64, device=red_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             want = int(t.item())
-        while prewarm_epochs < want:
-            wp, _, _ = one_step(wp, prewarm_epochs + 1)
-            prewarm_epochs += 1
+        if want > prewarm_epochs:
+            wp, _, _, _ = run_epochs(wp, prewarm_epochs + 1, want - prewarm_epochs)
+            prewarm_epochs = want
         torch.cuda.synchronize()
-        kernel_ms.clear()
     w = w0
-    for i in range(warmup):
-        w, cnt, loss = one_step(w, i + 1)
+    if warmup:
+        w, cnt, loss, _ = run_epochs(w, 1, warmup)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(steps)]
+    # one HIP event at each step's start and one after the last: each step's device time is the
+    # interval to the next start (an event pair per step cost the device ~5 us more per step)
+    events = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     if world > 1:
         engine.exchange_events = []   # HIP events around each timed step's all-gather + fold
+    first_launch = engine.ctx.chain_launches()
     t0 = time.perf_counter()
-    total = 0
-    for i in range(steps):
-        w, cnt, loss = one_step(w, warmup + i + 1, events[i])
-        total += cnt
+    w, cnt, loss, total = run_epochs(w, warmup + 1, steps, events)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -517,7 +547,8 @@ def run_workload(torch, dist, pkg, dev, rank, world, local, workload, compute, r
         samples_per_step = total / steps
     value = samples_per_step * steps / elapsed
     assert np.isfinite(loss), loss
-    epoch_ms = [a.elapsed_time(b) for a, b in events]
+    kernel_ms = chain_ms_since(first_launch)
+    epoch_ms = [a.elapsed_time(b) for a, b in zip(events[:-1], events[1:])]
     avg_epoch_s = sum(epoch_ms) / len(epoch_ms) / 1e3
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
     ranks = None

@@ -152,11 +152,23 @@ int32_t psgd_run_epoch(psgd_ctx* ctx, const psgd_params* params, const double* w
 int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const double* d_w_in,
                               double* d_partial, int64_t* d_chain_counts, void* stream);
 
+/* psgd_run_epoch_device whose fold kernel also writes {regVal, lossSum, (double)count} to
+ * h_scalars[3], page-locked host memory (psgd_host_alloc; nullable): no copy is enqueued. The
+ * count is stored last, with release order: a host that set h_scalars[2] to a value no count
+ * takes (e.g. -1) before the call may poll it and then read the other two; or it waits for an
+ * event recorded after the call. For a host loop that keeps several epochs in flight. */
+int32_t psgd_run_epoch_device_mirror(psgd_ctx* ctx, const psgd_params* params, const double* d_w_in,
+                                     double* d_partial, int64_t* d_chain_counts, void* stream,
+                                     double* h_scalars);
+
 /* Fold n per-process partials (each d+3 doubles, laid out back to back, in rank order) with
  * the reference's combiner (PSGD.scala:271-276) into d_out[d+3]: the cross-GPU level of the
- * treeReduce, applied after an all-gather of the partials. */
+ * treeReduce, applied after an all-gather of the partials. The _mirror form also writes the
+ * folded {regVal, lossSum, count} to h_scalars[3] as psgd_run_epoch_device_mirror does. */
 int32_t psgd_fold_partials_device(psgd_ctx* ctx, int32_t n, int32_t d, const double* d_partials,
                                   double* d_out, void* stream);
+int32_t psgd_fold_partials_device_mirror(psgd_ctx* ctx, int32_t n, int32_t d, const double* d_partials,
+                                         double* d_out, void* stream, double* h_scalars);
 
 /* Driver-side isConverged terms (PSGD.scala:289-294, :324-336): writes
  * {sum((prev-cur)^2), sum(cur^2)} to h_out[2] (host) after synchronising `stream`. */
@@ -186,6 +198,12 @@ int32_t psgd_ctx_last_kernel(psgd_ctx* ctx);
 /* Diagnostics: device time of the last chain-kernel launch in milliseconds, from HIP events
  * recorded around it on the launch stream (waits for that launch to finish). */
 int32_t psgd_ctx_last_chain_ms(psgd_ctx* ctx, double* ms_out);
+
+/* Diagnostics: the number of chain-kernel launches the context has made, and the device time of
+ * launch `launch` (0-based, one of the last 64; waits for it to finish) -- for a caller that
+ * keeps several epochs in flight and reads their times afterwards. */
+int64_t psgd_ctx_chain_launches(psgd_ctx* ctx);
+int32_t psgd_ctx_chain_ms(psgd_ctx* ctx, int64_t launch, double* ms_out);
 
 /* Diagnostics (no reference counterpart): process-wide counters of the virtual-memory mappings
  * that hold the CSR chains' large weight vectors (PSGD_VMM): out4[0] chunks mapped, [1] chunks

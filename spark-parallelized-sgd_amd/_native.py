@@ -23,8 +23,10 @@ EXPORTED = (
     "psgd_abi_version", "psgd_last_error", "psgd_ctx_create", "psgd_ctx_destroy",
     "psgd_register_dense", "psgd_register_csr", "psgd_register_dense_device", "psgd_register_csr_device",
     "psgd_clear_partitions", "psgd_num_partitions", "psgd_run_epoch", "psgd_run_epoch_device",
-    "psgd_fold_partials_device", "psgd_convergence_terms_device", "psgd_initial_regval",
-    "psgd_ctx_last_kernel", "psgd_ctx_last_chain_ms", "psgd_vmm_stats", "psgd_reroll_stats", "psgd_libsvm_read", "psgd_libsvm_free",
+    "psgd_fold_partials_device", "psgd_run_epoch_device_mirror", "psgd_fold_partials_device_mirror",
+    "psgd_convergence_terms_device", "psgd_initial_regval",
+    "psgd_ctx_last_kernel", "psgd_ctx_last_chain_ms", "psgd_ctx_chain_launches", "psgd_ctx_chain_ms",
+    "psgd_vmm_stats", "psgd_reroll_stats", "psgd_libsvm_read", "psgd_libsvm_free",
     "psgd_sample_partition", "psgd_host_alloc", "psgd_host_free", "psgd_register_wait",
 )
 
@@ -99,10 +101,14 @@ def lib():
             "psgd_run_epoch": ([vp, P, vp, vp, dp, dp, i64p, vp], C.c_int32),
             "psgd_run_epoch_device": ([vp, P, vp, vp, vp, vp], C.c_int32),
             "psgd_fold_partials_device": ([vp, C.c_int32, C.c_int32, vp, vp, vp], C.c_int32),
+            "psgd_run_epoch_device_mirror": ([vp, P, vp, vp, vp, vp, vp], C.c_int32),
+            "psgd_fold_partials_device_mirror": ([vp, C.c_int32, C.c_int32, vp, vp, vp, vp], C.c_int32),
             "psgd_convergence_terms_device": ([vp, C.c_int32, vp, vp, dp, vp], C.c_int32),
             "psgd_initial_regval": ([vp, P, C.c_int32, vp, dp], C.c_int32),
             "psgd_ctx_last_kernel": ([vp], C.c_int32),
             "psgd_ctx_last_chain_ms": ([vp, dp], C.c_int32),
+            "psgd_ctx_chain_launches": ([vp], C.c_int64),
+            "psgd_ctx_chain_ms": ([vp, C.c_int64, dp], C.c_int32),
             "psgd_vmm_stats": ([i64p], C.c_int32),
             "psgd_reroll_stats": ([i64p], C.c_int32),
             "psgd_libsvm_read": ([C.c_char_p, C.c_int32, C.c_int32, C.POINTER(C.POINTER(psgd_libsvm))], C.c_int32),
@@ -259,6 +265,16 @@ class Context:
         check(self._L.psgd_ctx_last_chain_ms(self.handle, C.byref(ms)))
         return ms.value
 
+    def chain_launches(self) -> int:
+        """Chain-kernel launches this context has made (the index of the next one)."""
+        return int(self._L.psgd_ctx_chain_launches(self.handle))
+
+    def chain_ms(self, launch: int) -> float:
+        """Device time of chain-kernel launch `launch` (0-based; one of the last 64)."""
+        ms = C.c_double()
+        check(self._L.psgd_ctx_chain_ms(self.handle, C.c_int64(launch), C.byref(ms)))
+        return ms.value
+
     # epochs ---------------------------------------------------------------------------------
     def run_epoch_device(self, params, w_ptr, partial_ptr, counts_ptr=None, stream=None):
         check(self._L.psgd_run_epoch_device(self.handle, C.byref(params), w_ptr, partial_ptr,
@@ -266,6 +282,16 @@ class Context:
 
     def fold_partials_device(self, n, d, partials_ptr, out_ptr, stream=None):
         check(self._L.psgd_fold_partials_device(self.handle, n, d, partials_ptr, out_ptr, stream))
+
+    def run_epoch_device_mirror(self, params, w_ptr, partial_ptr, counts_ptr, stream, h_ptr):
+        """run_epoch_device whose fold also writes {regVal, lossSum, count} to h_ptr[3]
+        (page-locked host memory, host_array)."""
+        check(self._L.psgd_run_epoch_device_mirror(self.handle, C.byref(params), w_ptr, partial_ptr,
+                                                   counts_ptr, stream, h_ptr))
+
+    def fold_partials_device_mirror(self, n, d, partials_ptr, out_ptr, stream, h_ptr):
+        check(self._L.psgd_fold_partials_device_mirror(self.handle, n, d, partials_ptr, out_ptr, stream,
+                                                       h_ptr))
 
     def convergence_terms_device(self, d, prev_ptr, cur_ptr, stream=None):
         out = (C.c_double * 2)()

@@ -423,9 +423,12 @@ struct psgd_ctx {
     double steps_value = NAN;
     int64_t steps_n = 0;
     int32_t last_variant = 0;
-    // HIP events around the last chain-kernel launch (psgd_ctx_last_chain_ms)
-    hipEvent_t ev_begin = nullptr, ev_end = nullptr;
-    bool ev_recorded = false;
+    // HIP events around the last kChainEvents chain-kernel launches, launch k in slot
+    // k % kChainEvents (psgd_ctx_last_chain_ms, psgd_ctx_chain_ms): a caller that keeps several
+    // epochs in flight reads each launch's time after it has enqueued later ones
+    static constexpr int kChainEvents = 64;
+    hipEvent_t ev_begin[kChainEvents] = {}, ev_end[kChainEvents] = {};
+    int64_t chain_launches = 0;
     // The scratch buffers above belong to the context, and epochs may run on different caller
     // streams: each user of them orders its stream after the previous user's work (this event,
     // recorded on `scratch_stream`) and records the event again when it has enqueued its own.
@@ -634,7 +637,11 @@ int32_t prepare(psgd_ctx* ctx, int32_t d, int state_vectors, hipStream_t st) {
     HIP_TRY(ctx->cnt.ensure(std::max<size_t>(P, 1) * sizeof(int64_t)));
     HIP_TRY(ctx->partial.ensure(((size_t)std::max(d, 1) + 3) * sizeof(double)));
     HIP_TRY(ctx->tmp.ensure(((size_t)std::max(d, 1) + 8) * sizeof(double)));
-    HIP_TRY(ctx->watchdog.ensure(16));
+    if (!ctx->watchdog.p) {
+        // zeroed once: from then on every epoch's fold kernel clears the flags it has read
+        HIP_TRY(ctx->watchdog.ensure(16));
+        HIP_TRY(hipMemsetAsync(ctx->watchdog.p, 0, 16, st));
+    }
     if (state_vectors > 0)
         HIP_TRY(ctx->state.ensure(std::max<size_t>(P, 1) * (size_t)state_vectors *
                                   (size_t)std::max(d, 1) * sizeof(double)));
@@ -762,8 +769,10 @@ int32_t psgd_ctx_destroy(psgd_ctx* ctx) {
                           &ctx->sdescs, &ctx->srows, &ctx->sys, &ctx->xstate,
                           &ctx->watchdog})
             b->release();
-        if (ctx->ev_begin) hipEventDestroy(ctx->ev_begin);
-        if (ctx->ev_end) hipEventDestroy(ctx->ev_end);
+        for (int k = 0; k < psgd_ctx::kChainEvents; ++k) {
+            if (ctx->ev_begin[k]) hipEventDestroy(ctx->ev_begin[k]);
+            if (ctx->ev_end[k]) hipEventDestroy(ctx->ev_end[k]);
+        }
         if (ctx->copy_ev) hipEventDestroy(ctx->copy_ev);
         if (ctx->scratch_ev) {
             hipEventSynchronize(ctx->scratch_ev);
@@ -1083,8 +1092,40 @@ int32_t psgd_num_partitions(psgd_ctx* ctx, int64_t* n_parts, int64_t* n_rows_tot
     return PSGD_OK;
 }
 
+// The host mirror's device address (page-locked memory from psgd_host_alloc / hipHostMalloc).
+static int32_t mirror_address(psgd_ctx* ctx, double* h, double** dev) {
+    *dev = nullptr;
+    if (!h) return PSGD_OK;
+    DeviceGuard g(ctx->device);
+    void* p = nullptr;
+    if (hipHostGetDevicePointer(&p, h, 0) != hipSuccess || !p) {
+        (void)hipGetLastError();
+        return fail(PSGD_EINVAL, "h_scalars is not page-locked host memory (psgd_host_alloc)");
+    }
+    *dev = static_cast<double*>(p);
+    return PSGD_OK;
+}
+
+static int32_t run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const double* d_w_in,
+                                double* d_partial, int64_t* d_chain_counts, void* stream, double* mirror);
+
 int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const double* d_w_in,
                               double* d_partial, int64_t* d_chain_counts, void* stream) {
+    return run_epoch_device(ctx, params, d_w_in, d_partial, d_chain_counts, stream, nullptr);
+}
+
+int32_t psgd_run_epoch_device_mirror(psgd_ctx* ctx, const psgd_params* params, const double* d_w_in,
+                                     double* d_partial, int64_t* d_chain_counts, void* stream,
+                                     double* h_scalars) {
+    if (!ctx) return fail(PSGD_EINVAL, "ctx is null");
+    double* mirror = nullptr;
+    int32_t rc = mirror_address(ctx, h_scalars, &mirror);
+    if (rc) return rc;
+    return run_epoch_device(ctx, params, d_w_in, d_partial, d_chain_counts, stream, mirror);
+}
+
+static int32_t run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const double* d_w_in,
+                                double* d_partial, int64_t* d_chain_counts, void* stream, double* mirror) {
     if (!ctx) return fail(PSGD_EINVAL, "ctx is null");
     int32_t rc = validate_params(params);
     if (rc) return rc;
@@ -1250,7 +1291,6 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         HIP_TRY(ctx->zbuf.ensure((size_t)P * (size_t)L.zstride * sizeof(double)));
         L.zbuf64 = ctx->zbuf.as<double>();
     }
-    HIP_TRY(hipMemsetAsync(L.watchdog, 0, 16, st));
     psgd::KParams kp;
     kp.reg = params->reg_param;
     kp.tol = params->convergence_tol;
@@ -1274,18 +1314,19 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
         HIP_TRY(hipMemsetAsync(L.cnt_d, 0, P * sizeof(double), st));
         HIP_TRY(hipMemsetAsync(L.cnt, 0, P * sizeof(int64_t), st));
     } else {
-        if (!ctx->ev_begin) {
-            HIP_TRY(hipEventCreate(&ctx->ev_begin));
-            HIP_TRY(hipEventCreate(&ctx->ev_end));
+        const int ek = (int)(ctx->chain_launches % psgd_ctx::kChainEvents);
+        if (!ctx->ev_begin[ek]) {
+            HIP_TRY(hipEventCreate(&ctx->ev_begin[ek]));
+            HIP_TRY(hipEventCreate(&ctx->ev_end[ek]));
         }
-        HIP_TRY(hipEventRecord(ctx->ev_begin, st));
+        HIP_TRY(hipEventRecord(ctx->ev_begin[ek], st));
         int e = psgd::launch_chains(L, kp, layout, first.dtype == PSGD_F32 ? 1 : 0,
                                     params->compute_dtype == PSGD_F32 ? 1 : 0, params->gradient,
                                     params->updater, conv, min_ld, max_ld,
                                     lds_spread_bytes(ctx, (size_t)P), st, &ctx->last_variant, max_nnz,
                                     &weights_in);
-        HIP_TRY(hipEventRecord(ctx->ev_end, st));
-        ctx->ev_recorded = (e == 0);
+        HIP_TRY(hipEventRecord(ctx->ev_end[ek], st));
+        if (e == 0) ++ctx->chain_launches;
         if (L.stamps) {   // PSGD_STAMPS=1: per-chain cycle counters of the CSR fp32 kernels (stderr)
             // chain_sparse_lds: {chain, loader, tagger} x {total, waiting}; chain_sparse_spec:
             // {chain, helper} x {total, waiting}
@@ -1312,19 +1353,26 @@ int32_t psgd_run_epoch_device(psgd_ctx* ctx, const psgd_params* params, const do
                         split ? nm : KS == 6 ? n6[k] : n4[k], v[k][v[k].size() / 2]);
             }
         }
-        if (e == -2) return fail(PSGD_EUNSUPPORTED, "this gradient/updater/layout combination is not built");
-        if (e) return fail(PSGD_EDEVICE, std::string("chain kernel launch failed: ") +
-                                             hipGetErrorString((hipError_t)e));
+        if (e) {
+            // (no fold clears the flags of a kernel that launched before the failure)
+            (void)hipMemsetAsync(L.watchdog, 0, 16, st);
+            if (e == -2) return fail(PSGD_EUNSUPPORTED, "this gradient/updater/layout combination is not built");
+            return fail(PSGD_EDEVICE, std::string("chain kernel launch failed: ") + hipGetErrorString((hipError_t)e));
+        }
     }
     // the CSR kernels of L.wf32 leave each chain's weights there (w = alpha v, floats or doubles)
     int e = weights_in == psgd::kWeightsF32
                 ? psgd::launch_fold_f32(L.wf32, L.wstride, L.walpha, L.rv, L.loss, L.cnt_d, P, dw, d_partial,
-                                        L.watchdog, st)
+                                        L.watchdog, st, mirror)
             : weights_in == psgd::kWeightsF64
                 ? psgd::launch_fold_f64(reinterpret_cast<const double*>(L.wf32), L.wstride / 2, L.walpha, L.rv,
-                                        L.loss, L.cnt_d, P, dw, d_partial, L.watchdog, st)
-                : psgd::launch_fold(L.w_out, dw, L.rv, L.loss, L.cnt_d, 1, P, dw, d_partial, L.watchdog, st);
-    if (e) return fail(PSGD_EDEVICE, "fold kernel launch failed");
+                                        L.loss, L.cnt_d, P, dw, d_partial, L.watchdog, st, mirror)
+                : psgd::launch_fold(L.w_out, dw, L.rv, L.loss, L.cnt_d, 1, P, dw, d_partial, L.watchdog, st,
+                                    mirror);
+    if (e) {
+        (void)hipMemsetAsync(L.watchdog, 0, 16, st);
+        return fail(PSGD_EDEVICE, "fold kernel launch failed");
+    }
     if (d_chain_counts)
         HIP_TRY(hipMemcpyAsync(d_chain_counts, L.cnt, (size_t)P * sizeof(int64_t),
                                hipMemcpyDeviceToDevice, st));
@@ -1384,17 +1432,25 @@ int32_t psgd_run_epoch(psgd_ctx* ctx, const psgd_params* params, const double* w
     return PSGD_OK;
 }
 
-int32_t psgd_fold_partials_device(psgd_ctx* ctx, int32_t n, int32_t d, const double* d_partials,
-                                  double* d_out, void* stream) {
+int32_t psgd_fold_partials_device_mirror(psgd_ctx* ctx, int32_t n, int32_t d, const double* d_partials,
+                                         double* d_out, void* stream, double* h_scalars) {
     if (!ctx) return fail(PSGD_EINVAL, "ctx is null");
     if (n <= 0 || d <= 0 || !d_partials || !d_out) return fail(PSGD_EINVAL, "bad fold arguments");
+    double* mirror = nullptr;
+    int32_t rc = mirror_address(ctx, h_scalars, &mirror);
+    if (rc) return rc;
     DeviceGuard g(ctx->device);
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     const int64_t stride = (int64_t)d + 3;
     int e = psgd::launch_fold(d_partials, stride, d_partials + d, d_partials + d + 1,
-                              d_partials + d + 2, stride, n, d, d_out, nullptr, st);
+                              d_partials + d + 2, stride, n, d, d_out, nullptr, st, mirror);
     if (e) return fail(PSGD_EDEVICE, "fold kernel launch failed");
     return PSGD_OK;
+}
+
+int32_t psgd_fold_partials_device(psgd_ctx* ctx, int32_t n, int32_t d, const double* d_partials,
+                                  double* d_out, void* stream) {
+    return psgd_fold_partials_device_mirror(ctx, n, d, d_partials, d_out, stream, nullptr);
 }
 
 int32_t psgd_convergence_terms_device(psgd_ctx* ctx, int32_t d, const double* d_prev,
@@ -1486,16 +1542,29 @@ int32_t psgd_sample_partition(int32_t device, int64_t seed, int64_t n, double fr
 
 int32_t psgd_ctx_last_kernel(psgd_ctx* ctx) { return ctx ? ctx->last_variant : 0; }
 
-int32_t psgd_ctx_last_chain_ms(psgd_ctx* ctx, double* ms_out) {
+int32_t psgd_ctx_chain_ms(psgd_ctx* ctx, int64_t launch, double* ms_out) {
     if (!ctx || !ms_out) return fail(PSGD_EINVAL, "ctx/ms_out is null");
-    if (!ctx->ev_recorded) return fail(PSGD_ESTATE, "no chain kernel has been launched");
+    if (ctx->chain_launches == 0) return fail(PSGD_ESTATE, "no chain kernel has been launched");
+    if (launch < 0 || launch >= ctx->chain_launches || launch < ctx->chain_launches - psgd_ctx::kChainEvents)
+        return fail(PSGD_EINVAL, "launch " + std::to_string(launch) + " is not among the last " +
+                                     std::to_string(psgd_ctx::kChainEvents) + " of " +
+                                     std::to_string(ctx->chain_launches));
     DeviceGuard g(ctx->device);
-    HIP_TRY(hipEventSynchronize(ctx->ev_end));
+    const int ek = (int)(launch % psgd_ctx::kChainEvents);
+    HIP_TRY(hipEventSynchronize(ctx->ev_end[ek]));
     float ms = 0.0f;
-    HIP_TRY(hipEventElapsedTime(&ms, ctx->ev_begin, ctx->ev_end));
+    HIP_TRY(hipEventElapsedTime(&ms, ctx->ev_begin[ek], ctx->ev_end[ek]));
     *ms_out = ms;
     return PSGD_OK;
 }
+
+int32_t psgd_ctx_last_chain_ms(psgd_ctx* ctx, double* ms_out) {
+    if (!ctx || !ms_out) return fail(PSGD_EINVAL, "ctx/ms_out is null");
+    if (ctx->chain_launches == 0) return fail(PSGD_ESTATE, "no chain kernel has been launched");
+    return psgd_ctx_chain_ms(ctx, ctx->chain_launches - 1, ms_out);
+}
+
+int64_t psgd_ctx_chain_launches(psgd_ctx* ctx) { return ctx ? ctx->chain_launches : 0; }
 
 int32_t psgd_vmm_stats(int64_t* out4) {
     if (!out4) return fail(PSGD_EINVAL, "out4 is null");

@@ -106,13 +106,16 @@ int launch_block64_chains(const ChainLaunch& L, const KParams& kp, int storage, 
 int launch_logistic_loss64(const ChainLaunch& L, int n_chains, hipStream_t stream);
 // lossSum of fp32 Logistic chains from the per-row margins in L.zbuf (psgd_block.hip).
 int launch_margin_loss(const ChainLaunch& L, int n_chains, hipStream_t stream);
+// The fold kernels read the epoch's watchdog flags (a set flag poisons the count) and clear them
+// for the next epoch; mirror (nullable, device-visible page-locked host memory) also receives
+// {regVal, lossSum, count}.
 int launch_fold(const double* w, int64_t w_stride, const double* rv, const double* loss,
                 const double* cnt, int64_t s_stride, int n, int d, double* out,
-                const int* watchdog, hipStream_t stream);
+                int* watchdog, hipStream_t stream, double* mirror = nullptr);
 // The combiner over the CSR fp32 kernels' outputs: w_p = walpha[p] * double(wf32[p][i]).
 int launch_fold_f32(const float* wf32, int64_t wstride, const double* walpha, const double* rv,
                     const double* loss, const double* cnt, int n, int d, double* out,
-                    const int* watchdog, hipStream_t stream);
+                    int* watchdog, hipStream_t stream, double* mirror = nullptr);
 int launch_sq_terms(const double* a, const double* b, int d, double* out2, hipStream_t stream);
 int launch_steps(double step, int64_t n, double* steps, hipStream_t stream);
 // The fp32 CSR kernel (psgd_sparse.hip): weights as fp32 vectors in HBM (L.wf32).
@@ -132,7 +135,7 @@ int launch_sparse64_chains(const ChainLaunch& L, const KParams& kp, int storage,
 // The combiner over chain_sparse64's vectors: w_p = walpha[p] * v_p[i] (v_p doubles).
 int launch_fold_f64(const double* wv, int64_t wstride_d, const double* walpha, const double* rv,
                     const double* loss, const double* cnt, int n, int d, double* out,
-                    const int* watchdog, hipStream_t stream);
+                    int* watchdog, hipStream_t stream, double* mirror = nullptr);
 // The fp32 CSR kernel with LDS-resident weights (psgd_sparse_lds.hip): rows of <= 128 non-zeros,
 // features [0, K) in LDS and [K, d) in L.wf32; -3 when it does not apply.
 bool sparse_lds_applies(int64_t d, int64_t max_nnz, int64_t n_max);

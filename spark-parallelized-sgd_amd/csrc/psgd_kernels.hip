@@ -668,39 +668,130 @@ __global__ __launch_bounds__(64) void chain_general(ChainLaunch L, KParams kp) {
 }
 
 // ------------------------------------------------------------------------------------------
-// fold_kernel: the reference combiner (PSGD.scala:271-276) as a left fold over n items in
-// index order, one thread per coordinate; the thread with i == d folds the scalars.
+// The reference combiner (PSGD.scala:271-276) as a left fold over n items in index order, one
+// thread per coordinate; the thread with i == d folds the scalars.
 //   w = (w1*c1 + w2*c2) / (c1 + c2);  rv likewise;  loss = l1 + l2;  c = c1 + c2
 // out[0..d) = w, out[d] = regVal, out[d+1] = lossSum, out[d+2] = count.
+//
+// Each step is one dependent f64 multiply, add and IEEE division on the coordinate's running
+// value; the item loads are not on that chain. Loading item p at its step (round 6 and before)
+// left the steps waiting on memory round trips: 40 us per c2 epoch (256 chains, d = 512) for
+// ~10 us of dependent arithmetic. Now the block stages the per-item scalars (counts, and regVal,
+// loss, alpha as needed) in LDS, kFoldStage items at a time, and every coordinate thread keeps
+// its next kFoldAhead weights in flight while it folds the current ones. Same operations in
+// the same order: bit-identical results.
 // ------------------------------------------------------------------------------------------
-__global__ void fold_kernel(const double* __restrict__ w, int64_t w_stride,
-                            const double* __restrict__ rv, const double* __restrict__ loss,
-                            const double* __restrict__ cnt, int64_t s_stride, int n, int d,
-                            double* __restrict__ out, const int* __restrict__ watchdog) {
+constexpr int kFoldStage = 512;    // items staged in LDS at a time
+constexpr int kFoldAhead = 16;     // weight loads in flight per coordinate thread
+constexpr int kFoldThreads = 256;
+
+// WLOAD(p, a) -> item p's weight for this thread's coordinate (a = item p's alpha, if staged)
+template <bool ALPHA, typename WLoad>
+__device__ __forceinline__ void fold_items(WLoad wload, const double* __restrict__ alpha,
+                                           const double* __restrict__ rv, const double* __restrict__ loss,
+                                           const double* __restrict__ cnt, int64_t s_stride, int n, int d,
+                                           double* __restrict__ out, int* __restrict__ watchdog,
+                                           double* __restrict__ mirror) {
+    __shared__ double sc[kFoldStage], sr[kFoldStage], sl[kFoldStage], sa[ALPHA ? kFoldStage : 1];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < d) {
-        double acc = w[i];
-        double c1 = cnt[0];
-#pragma unroll 16
-        for (int p = 1; p < n; ++p) {
-            const double c2 = cnt[p * s_stride];
-            acc = (acc * c1 + w[p * w_stride + i] * c2) / (c1 + c2);
-            c1 = c1 + c2;
+    const bool wt = i < d;                                   // a weight coordinate
+    const bool st = i == d;                                  // the scalars
+    const bool blk_st = (int)(blockIdx.x * blockDim.x) <= d && d < (int)((blockIdx.x + 1) * blockDim.x);
+    double acc = 0.0, r = 0.0, l = 0.0, c1 = 0.0;
+    for (int s0 = 0; s0 < n; s0 += kFoldStage) {
+        const int m = n - s0 < kFoldStage ? n - s0 : kFoldStage;
+        __syncthreads();   // the previous stage's items are folded
+        for (int k = threadIdx.x; k < m; k += blockDim.x) {
+            const int64_t q = (int64_t)(s0 + k) * s_stride;
+            sc[k] = cnt[q];
+            if (blk_st) {
+                sr[k] = rv[q];
+                sl[k] = loss[q];
+            }
+            if constexpr (ALPHA) sa[k] = alpha[s0 + k];
         }
+        __syncthreads();
+        const int k0 = s0 == 0 ? 1 : 0;   // item 0 starts the fold
+        if (s0 == 0) {
+            c1 = sc[0];
+            if (wt) acc = wload(0, ALPHA ? sa[0] : 1.0);
+            if (st) {
+                r = sr[0];
+                l = sl[0];
+            }
+        }
+        if (wt) {
+            // items [k0, m) of the stage, kFoldAhead at a time, the next group's loads issued
+            // before the current group's steps (indices clamped to the stage: a group past its
+            // end loads item m - 1 again and folds nothing)
+            double cur[kFoldAhead], nxt[kFoldAhead];
+            auto fetch = [&](double (&v)[kFoldAhead], int g0) __attribute__((always_inline)) {
+#pragma unroll
+                for (int j = 0; j < kFoldAhead; ++j) {
+                    const int k = g0 + j < m ? g0 + j : m - 1;
+                    v[j] = wload(s0 + k, ALPHA ? sa[k] : 1.0);
+                }
+            };
+            fetch(cur, k0);
+            for (int g0 = k0; g0 < m; g0 += kFoldAhead) {
+                fetch(nxt, g0 + kFoldAhead);
+#pragma unroll
+                for (int j = 0; j < kFoldAhead; ++j) {
+                    if (g0 + j < m) {
+                        const double c2 = sc[g0 + j];
+                        acc = (acc * c1 + cur[j] * c2) / (c1 + c2);
+                        c1 = c1 + c2;
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < kFoldAhead; ++j) cur[j] = nxt[j];
+            }
+        } else if (st) {
+            for (int k = k0; k < m; ++k) {
+                const double c2 = sc[k];
+                r = (r * c1 + sr[k] * c2) / (c1 + c2);
+                l = l + sl[k];
+                c1 = c1 + c2;
+            }
+        }
+    }
+    if (wt) {
         out[i] = acc;
-    } else if (i == d) {
-        double r = rv[0], l = loss[0], c1 = cnt[0];
-        for (int p = 1; p < n; ++p) {
-            const double c2 = cnt[p * s_stride];
-            r = (r * c1 + rv[p * s_stride] * c2) / (c1 + c2);
-            l = l + loss[p * s_stride];
-            c1 = c1 + c2;
+    } else if (st) {
+        // a chain kernel that tripped its watchdog poisons the count: the host raises. The
+        // flags are cleared here for the next epoch (every epoch's chains end in one fold), so
+        // the epoch enqueues no memset of its own
+        bool fired = false;
+        if (watchdog) {
+            fired = watchdog[0] != 0;   // (the chains' flags are OR-ed into word 0)
+            watchdog[0] = watchdog[1] = watchdog[2] = watchdog[3] = 0;
         }
+        const double cnt_out = fired ? __builtin_nan("") : c1;
         out[d] = r;
         out[d + 1] = l;
-        // a chain kernel that tripped its watchdog poisons the count: the host raises
-        out[d + 2] = (watchdog && *watchdog) ? __builtin_nan("") : c1;
+        out[d + 2] = cnt_out;
+        if (mirror) {
+            // the host's copy, system-scope stores; the count last, with release order, so a
+            // host that polls it (for a value other than the one it left there) then reads the
+            // other two finds them written
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(mirror), (unsigned long long)__double_as_longlong(r),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(mirror) + 1, (unsigned long long)__double_as_longlong(l),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(mirror) + 2,
+                               (unsigned long long)__double_as_longlong(cnt_out), __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
+}
+
+__global__ __launch_bounds__(kFoldThreads) void fold_kernel(const double* __restrict__ w, int64_t w_stride,
+                            const double* __restrict__ rv, const double* __restrict__ loss,
+                            const double* __restrict__ cnt, int64_t s_stride, int n, int d,
+                            double* __restrict__ out, int* __restrict__ watchdog, double* __restrict__ mirror) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    fold_items<false>([&](int p, double) { return w[(int64_t)p * w_stride + i]; }, nullptr, rv, loss, cnt,
+                      s_stride, n, d, out, watchdog, mirror);
 }
 
 // The same combiner over the fp32 CSR chains' weights, w_p = walpha[p] * double(v_p[i]) -- the
@@ -709,54 +800,35 @@ __global__ void fold_kernel(const double* __restrict__ w, int64_t w_stride,
 // (V = double: chain_sparse64's vectors, the same combiner with w_p = walpha[p] * v_p[i] -- the
 // value chain_general's W[i] = alpha * W[i] writes at the chain's end.)
 template <typename V>
-__global__ void fold_scaled_kernel(const V* __restrict__ v, int64_t v_stride,
+__global__ __launch_bounds__(kFoldThreads) void fold_scaled_kernel(const V* __restrict__ v, int64_t v_stride,
                                 const double* __restrict__ alpha, const double* __restrict__ rv,
                                 const double* __restrict__ loss, const double* __restrict__ cnt,
-                                int n, int d, double* __restrict__ out, const int* __restrict__ watchdog) {
+                                int n, int d, double* __restrict__ out, int* __restrict__ watchdog,
+                                double* __restrict__ mirror) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < d) {
-        double acc = alpha[0] * double(v[i]);
-        double c1 = cnt[0];
-#pragma unroll 16
-        for (int p = 1; p < n; ++p) {
-            const double c2 = cnt[p];
-            acc = (acc * c1 + alpha[p] * double(v[p * v_stride + i]) * c2) / (c1 + c2);
-            c1 = c1 + c2;
-        }
-        out[i] = acc;
-    } else if (i == d) {
-        double r = rv[0], l = loss[0], c1 = cnt[0];
-        for (int p = 1; p < n; ++p) {
-            const double c2 = cnt[p];
-            r = (r * c1 + rv[p] * c2) / (c1 + c2);
-            l = l + loss[p];
-            c1 = c1 + c2;
-        }
-        out[d] = r;
-        out[d + 1] = l;
-        out[d + 2] = (watchdog && *watchdog) ? __builtin_nan("") : c1;
-    }
+    fold_items<true>([&](int p, double a) { return a * double(v[(int64_t)p * v_stride + i]); }, alpha, rv, loss,
+                     cnt, 1, n, d, out, watchdog, mirror);
 }
 
 int launch_fold_f32(const float* wf32, int64_t wstride, const double* walpha, const double* rv,
                     const double* loss, const double* cnt, int n, int d, double* out,
-                    const int* watchdog, hipStream_t stream) {
+                    int* watchdog, hipStream_t stream, double* mirror) {
     if (n <= 0) return -1;
-    const int threads = 256;
+    const int threads = kFoldThreads;
     const int blocks = (d + 1 + threads - 1) / threads;
     hipLaunchKernelGGL(fold_scaled_kernel<float>, dim3(blocks), dim3(threads), 0, stream, wf32, wstride, walpha,
-                       rv, loss, cnt, n, d, out, watchdog);
+                       rv, loss, cnt, n, d, out, watchdog, mirror);
     return (int)hipGetLastError();
 }
 
 int launch_fold_f64(const double* wv, int64_t wstride_d, const double* walpha, const double* rv,
                     const double* loss, const double* cnt, int n, int d, double* out,
-                    const int* watchdog, hipStream_t stream) {
+                    int* watchdog, hipStream_t stream, double* mirror) {
     if (n <= 0) return -1;
-    const int threads = 256;
+    const int threads = kFoldThreads;
     const int blocks = (d + 1 + threads - 1) / threads;
     hipLaunchKernelGGL(fold_scaled_kernel<double>, dim3(blocks), dim3(threads), 0, stream, wv, wstride_d, walpha,
-                       rv, loss, cnt, n, d, out, watchdog);
+                       rv, loss, cnt, n, d, out, watchdog, mirror);
     return (int)hipGetLastError();
 }
 
@@ -1002,12 +1074,12 @@ int launch_chains(const ChainLaunch& L, const KParams& kp, int layout, int stora
 
 int launch_fold(const double* w, int64_t w_stride, const double* rv, const double* loss,
                 const double* cnt, int64_t s_stride, int n, int d, double* out,
-                const int* watchdog, hipStream_t stream) {
+                int* watchdog, hipStream_t stream, double* mirror) {
     if (n <= 0) return -1;
-    const int threads = 256;
+    const int threads = kFoldThreads;
     const int blocks = (d + 1 + threads - 1) / threads;
     hipLaunchKernelGGL(fold_kernel, dim3(blocks), dim3(threads), 0, stream, w, w_stride, rv, loss,
-                       cnt, s_stride, n, d, out, watchdog);
+                       cnt, s_stride, n, d, out, watchdog, mirror);
     return (int)hipGetLastError();
 }
 

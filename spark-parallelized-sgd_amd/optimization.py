@@ -16,9 +16,11 @@ RCCL and the same fold in rank order (the cross-GPU level of the treeReduce).
 """
 from __future__ import annotations
 
+import collections
 import logging
 import math
 import threading
+import time
 import uuid
 from typing import List, Optional, Tuple
 
@@ -159,9 +161,13 @@ class HipEngine(ShardedEngine):
         self.ctx = get_context(device)
         # a real stream handle: NULL would select the library's own stream
         self.stream = torch.cuda.Stream(device=self.dev)
-        self._partial = torch.empty(self.d + 3, dtype=torch.float64, device=self.dev)
+        # two of each result buffer, alternating by epoch: an epoch's folded weights stay intact
+        # while the next epoch, which reads them, runs (adopt_view)
+        self._partials = [torch.empty(self.d + 3, dtype=torch.float64, device=self.dev) for _ in range(2)]
+        self._folds = [torch.empty(self.d + 3, dtype=torch.float64, device=self.dev) for _ in range(2)]
+        self._slot = 0
+        self._partial, self._folded = self._partials[0], self._folds[0]
         self._gather = torch.empty(self.world * (self.d + 3), dtype=torch.float64, device=self.dev)
-        self._folded = torch.empty(self.d + 3, dtype=torch.float64, device=self.dev)
         self._counts = torch.empty(max(self.n_local, 1), dtype=torch.int64, device=self.dev)
         self._data = data
         with self.ctx.engine_lock:
@@ -217,10 +223,16 @@ class HipEngine(ShardedEngine):
         caller = self.torch.cuda.current_stream(self.dev)
         # order after whatever produced the inputs on the caller's stream
         self.stream.wait_stream(caller)
-        with self.torch.cuda.stream(self.stream):
-            out = super().epoch(params, w_dev, with_counts)
+        out = self._enqueue(params, w_dev, with_counts)
         caller.wait_stream(self.stream)
         return out
+
+    def _enqueue(self, params, w_dev, with_counts=False):
+        """The epoch on self.stream (into the next pair of result buffers), no cross-stream order."""
+        self._slot ^= 1
+        self._partial, self._folded = self._partials[self._slot], self._folds[self._slot]
+        with self.torch.cuda.stream(self.stream):
+            return super().epoch(params, w_dev, with_counts)
 
     def local_partial(self, params, w_dev, with_counts):
         # The lock serialises re-registration and the enqueue; the device order of epochs that
@@ -230,9 +242,14 @@ class HipEngine(ShardedEngine):
             # another engine on this device may have registered its own partitions since
             if self.ctx.registered_token != self._key:
                 self._register(self._data)
-            self.ctx.run_epoch_device(params, w_dev.data_ptr(), self._partial.data_ptr(),
-                                      self._counts.data_ptr() if with_counts else None,
-                                      self.stream.cuda_stream)
+            counts_ptr = self._counts.data_ptr() if with_counts else None
+            if self._mirror_next is not None and self.world == 1:
+                self.ctx.run_epoch_device_mirror(params, w_dev.data_ptr(), self._partial.data_ptr(), counts_ptr,
+                                                 self.stream.cuda_stream, self._mirror_next)
+                self._mirror_used = True
+            else:
+                self.ctx.run_epoch_device(params, w_dev.data_ptr(), self._partial.data_ptr(), counts_ptr,
+                                          self.stream.cuda_stream)
         counts = self._counts[: self.n_local].cpu().numpy() if with_counts else None
         return self._partial, counts
 
@@ -260,8 +277,13 @@ class HipEngine(ShardedEngine):
         return out
 
     def fold_partials(self, gathered):
-        self.ctx.fold_partials_device(self.world, self.d, gathered.data_ptr(),
-                                      self._folded.data_ptr(), self.stream.cuda_stream)
+        if self._mirror_next is not None:
+            self.ctx.fold_partials_device_mirror(self.world, self.d, gathered.data_ptr(), self._folded.data_ptr(),
+                                                 self.stream.cuda_stream, self._mirror_next)
+            self._mirror_used = True
+        else:
+            self.ctx.fold_partials_device(self.world, self.d, gathered.data_ptr(),
+                                          self._folded.data_ptr(), self.stream.cuda_stream)
         return self._folded
 
     def scalars(self, folded) -> Tuple[float, float, int]:
@@ -274,6 +296,76 @@ class HipEngine(ShardedEngine):
     def adopt(self, folded):
         with self.torch.cuda.stream(self.stream):
             return folded[: self.d].clone()
+
+    # the driver's pipelined loop (ParallelizedSGD._run_pipelined) ------------------------------
+    # An epoch's three scalars reach the host without a copy: the epoch's last fold kernel writes
+    # them to a page-locked slot as well (psgd_run_epoch_device_mirror /
+    # psgd_fold_partials_device_mirror); the host reads the slot after the epoch's event.
+    _PIN_SLOTS = 16
+    _mirror = None
+    _mirror_next = None
+    _mirror_used = False
+
+    def epoch_async(self, params, w_dev):
+        """epoch() that returns (folded, token) at once; scalars_wait(token) gives its scalars.
+        Tokens are read in the order they were made, fewer than _PIN_SLOTS behind the newest.
+        Unlike epoch() it orders nothing against the caller's stream (each cross-stream wait
+        costs the device ~20 us between epochs): w_dev must have been produced on self.stream
+        (weights(), adopt(), adopt_view() all are), and `folded` is read on self.stream or after
+        scalars_wait(token)."""
+        if self._mirror is None:
+            self._mirror = self.ctx.host_array((self._PIN_SLOTS, 3), np.float64)
+            self._pin_owner = [-1] * self._PIN_SLOTS
+            self._pin_seq = 0
+        seq = self._pin_seq
+        k = seq % self._PIN_SLOTS
+        if self._pin_owner[k] >= 0:
+            self._poll(k)   # (a slot is reused only after its last epoch's fold has written it)
+        self._mirror[k, 2] = self._UNSET   # the fold's count replaces it (psgd.h)
+        self._mirror_next, self._mirror_used = self._mirror[k].ctypes.data, False
+        try:
+            folded, _ = self._enqueue(params, w_dev)
+        finally:
+            used, self._mirror_next = self._mirror_used, None
+        if not used:   # (no fold of this epoch ran on this rank's context: copy the scalars)
+            with self.torch.cuda.stream(self.stream):
+                self.torch.from_numpy(self._mirror[k]).copy_(folded[self.d:])
+        self._pin_owner[k] = seq
+        self._pin_seq = seq + 1
+        return folded, (seq, k)
+
+    _UNSET = -1.0            # no count is negative
+    _WAIT_LIMIT_S = 600.0    # a chain kernel's own watchdog ends a stalled epoch in seconds
+
+    def scalars_wait(self, token) -> Tuple[float, float, int]:
+        """scalars() of the epoch behind `token`: polls its slot until the fold kernel's count
+        lands (no event: each event recorded between epochs costs the device a few us)."""
+        seq, k = token
+        if self._pin_owner[k] != seq:
+            raise RuntimeError(f"the scalars of epoch token {seq} were overwritten before they were read")
+        self._poll(k)
+        h = self._mirror[k].copy()
+        if not math.isfinite(h[2]):
+            raise N.DeviceError("chain kernel watchdog fired (loader/compute waves stalled)")
+        return float(h[0]), float(h[1]), int(h[2])
+
+    def _poll(self, k):
+        slot = self._mirror[k]
+        if slot[2] != self._UNSET:
+            return
+        t0 = time.perf_counter()
+        spins = 0
+        while slot[2] == self._UNSET:
+            spins += 1
+            if spins > 2000:   # past the first ~ms: yield between polls
+                time.sleep(20e-6)
+                if time.perf_counter() - t0 > self._WAIT_LIMIT_S:
+                    raise N.DeviceError("an epoch's fold did not complete")
+
+    def adopt_view(self, folded):
+        """adopt() without the copy: the folded weights in place, intact until the second epoch
+        after the one that produced them is enqueued (the result buffers alternate)."""
+        return folded[: self.d]
 
     def convergence_terms(self, prev, cur) -> Tuple[float, float]:
         return self.ctx.convergence_terms_device(self.d, prev.data_ptr(), cur.data_ptr(),
@@ -413,6 +505,11 @@ class ParallelizedSGD:
             have_current, converged, i = state["have_current"], state["converged"], state["i"]
             log.warning("resuming at iteration %d from checkpoint %s", i, checkpoint)
         last_saved = i
+        if (convergenceTol == 0.0 and miniBatchFraction >= 1.0 and ckpt is None and not return_chain_counts
+                and hasattr(engine, "epoch_async")):
+            weights, regVal = ParallelizedSGD._run_pipelined(engine, params, weights, regVal, i,
+                                                             numIterations, history)
+            i = numIterations + 1
         while not converged and i <= numIterations:       # :237
             params.iteration = i
             folded, counts = engine.epoch(params, weights, with_counts=return_chain_counts)
@@ -440,6 +537,47 @@ class ParallelizedSGD:
                  ", ".join(str(v) for v in history[-10:]))
         out = (engine.to_host(weights), np.array(history))
         return out + (chain_counts,) if return_chain_counts else out
+
+
+    # (the number of epochs enqueued ahead of the one whose scalars are read)
+    PIPELINE_LAG = 2
+
+    @staticmethod
+    def _run_pipelined(engine, params, weights, regVal: float, i: int, numIterations: int,
+                       history: List[float]):
+        """The loop :237-297 when its branches are known before an epoch's scalars are: with
+        convergenceTol == 0 `isConverged` (:324-336) is `norm < 0.0 * max(.)`, never true, and
+        with miniBatchFraction == 1 every row of the (non-empty, :214-217) data is in every batch
+        (:242), so batchSize > 0 (:278) and the folded weights are always adopted (:286). Each
+        epoch is enqueued with the previous epoch's folded weights before that epoch's three
+        scalars are read back, up to PIPELINE_LAG epochs ahead, so the device runs epoch after
+        epoch without waiting for the host; the loss history, regVal lag (:283, :287) and log
+        lines follow in iteration order as each epoch's scalars arrive. Returns (weights, regVal)."""
+        pending = collections.deque()
+
+        def settle(regVal):
+            it, token = pending.popleft()
+            avgRegVal, lossSum, batchSize = engine.scalars_wait(token)
+            if batchSize <= 0:   # a full batch of non-empty data: cannot happen
+                raise RuntimeError(f"iteration {it}: an empty batch in a full-batch epoch")
+            stochasticLoss = lossSum / batchSize + regVal          # :283
+            history.append(stochasticLoss)
+            log.warning("stochastic loss at step%d: %s", it, stochasticLoss)
+            return avgRegVal                                       # :287
+
+        while i <= numIterations:
+            params.iteration = i
+            folded, token = engine.epoch_async(params, weights)
+            pending.append((i, token))
+            # (valid while the next epoch reads it; every later use is after its own epoch)
+            weights = engine.adopt_view(folded)                    # :286
+            if len(pending) > ParallelizedSGD.PIPELINE_LAG:
+                regVal = settle(regVal)
+            i += 1
+        while pending:
+            regVal = settle(regVal)
+        # the last epoch's weights, copied out of the alternating result buffers
+        return engine.adopt(weights), regVal
 
 
 _CKPT_VERSION = 1

@@ -60,7 +60,8 @@ def main():
             res[name + "_rccl"] = got
             # the same epoch read on the default stream, with no stream block (HipEngine.epoch
             # makes the caller's stream wait for the engine's): the partial as it ends the epoch
-            eng._partial.fill_(-7.0)
+            for b in eng._partials:   # (the result buffers alternate by epoch)
+                b.fill_(-7.0)
             torch.cuda.synchronize()
             partial, _ = eng.epoch(prm, w)
             res[name + "_default"] = partial.cpu().numpy()

@@ -149,3 +149,64 @@ def test_driver_zero_iterations(pkg):
     w, h = pkg.runParallelizedSGD(data, pkg.LogisticGradient(), pkg.SimpleSGDUpdater(), 1.0, 0,
                                   0.0, 1.0, [0.5, 0.5], engine=eng)
     assert list(w) == [0.5, 0.5] and len(h) == 0 and eng.calls == 0
+
+
+class PipelinedScriptedEngine(ScriptedEngine):
+    """ScriptedEngine with HipEngine's asynchronous epochs (epoch_async / scalars_wait /
+    adopt_view); logs the order of enqueues and reads."""
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.log = []
+
+    def epoch(self, params, w, with_counts=False):
+        self.log.append(("epoch", params.iteration, tuple(np.asarray(w, dtype=float))))
+        return super().epoch(params, w, with_counts)
+
+    def epoch_async(self, params, w):
+        f, _ = self.epoch(params, w)
+        return f, np.array(f)
+
+    def scalars_wait(self, token):
+        self.log.append(("wait",))
+        return self.scalars(token)
+
+    def adopt_view(self, f):
+        return f[: self.d]
+
+
+def _scripted_results(k):
+    return [np.array([1.0 + i, 2.0 - i, 0.1 * (i + 1), 3.0 + i, 4.0]) for i in range(k)]
+
+
+def test_driver_pipelined_matches_synchronous_loop(pkg):
+    """tol == 0 and miniBatchFraction == 1: the pipelined loop (ParallelizedSGD._run_pipelined)
+    gives the synchronous loop's weights and loss history (regVal lag :283, adoption :286), each
+    epoch runs on the previous epoch's folded weights, and epochs are enqueued PIPELINE_LAG ahead
+    of the scalar reads."""
+    data = pkg.PartitionedData.parallelize(np.ones(4), np.ones((4, 2)), 2)
+    args = (data, pkg.LogisticGradient(), pkg.SquaredL2SGDUpdater(), 1.0, 6, 0.1, 1.0, [0.5, -0.5], 0.0)
+    w_s, h_s = pkg.runParallelizedSGD(*args, engine=ScriptedEngine(_scripted_results(6), 2))
+    eng = PipelinedScriptedEngine(_scripted_results(6), 2)
+    w_p, h_p = pkg.runParallelizedSGD(*args, engine=eng)
+    assert list(w_p) == list(w_s) and list(h_p) == list(h_s) and len(h_p) == 6
+    epochs = [e for e in eng.log if e[0] == "epoch"]
+    assert [e[1] for e in epochs] == [1, 2, 3, 4, 5, 6]
+    assert epochs[0][2] == (0.5, -0.5)
+    for i in range(1, 6):   # epoch i+1 runs on epoch i's folded weights
+        assert epochs[i][2] == (1.0 + (i - 1), 2.0 - (i - 1))
+    lag = pkg.ParallelizedSGD.PIPELINE_LAG
+    kinds = [e[0] for e in eng.log]
+    assert kinds[: lag + 2] == ["epoch"] * (lag + 1) + ["wait"]
+    assert kinds.count("wait") == 6
+
+
+def test_driver_pipelined_only_when_branches_are_known(pkg):
+    """tol > 0 (isConverged may stop the loop), miniBatchFraction < 1 (a batch may be empty) or
+    per-iteration chain counts keep the synchronous loop: no asynchronous reads."""
+    data = pkg.PartitionedData.parallelize(np.ones(4), np.ones((4, 2)), 2)
+    for tol, frac, counts in ((0.001, 1.0, False), (0.0, 0.5, False), (0.0, 1.0, True)):
+        eng = PipelinedScriptedEngine(_scripted_results(3), 2, terms=(100.0, 1.0))
+        pkg.runParallelizedSGD(data, pkg.LogisticGradient(), pkg.SimpleSGDUpdater(), 1.0, 3, 0.0, frac,
+                               [0.0, 0.0], tol, engine=eng, return_chain_counts=counts)
+        assert ("wait",) not in eng.log and eng.calls == 3

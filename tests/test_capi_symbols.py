@@ -11,7 +11,7 @@ from conftest import ROOT, has_gpu
 
 def header_functions():
     src = open(os.path.join(ROOT, "include", "psgd.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int32_t|void|const char\*)\s+(psgd_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int32_t|int64_t|void|const char\*)\s+(psgd_\w+)\s*\(", src, re.M)))
 
 
 def test_header_matches_binding_table(pkg):

@@ -306,6 +306,12 @@ def test_hip_engine_two_ranks(tmp_path, pkg, oracle, P):
     assert [list(c) for c in c0] == [list(c[:lo1]) for c in cr[: len(c0)]]
     if P > 1:
         assert [list(c) for c in c1] == [list(c[lo1:]) for c in cr[: len(c1)]]
+    # the pipelined loop (tol = 0): 5 iterations, all rows every time
+    wr0, hr0, _ = oracle.run(oracle.Matrix(y, X), offs, "logistic", "squared_l2", 0.5, 5, 0.01, np.zeros(d),
+                             tol=0.0, groups=groups)
+    assert len(res["hp"]) == 5
+    assert_close(res["wp"], wr0, what=f"P={P} pipelined weights")
+    assert_close(res["hp"], hr0, what=f"P={P} pipelined loss")
 
 
 def test_rccl_exchange_single_rank(tmp_path):
@@ -348,7 +354,8 @@ def test_epoch_result_on_default_stream(pkg):
     w = eng.weights(np.zeros(d))
     ref = None
     for _ in range(3):
-        eng._partial.fill_(-7.0)
+        for b in eng._partials:   # (the result buffers alternate by epoch)
+            b.fill_(-7.0)
         torch.cuda.synchronize()
         partial, _ = eng.epoch(prm, w)
         got = partial.cpu().numpy()          # the default stream, no stream block

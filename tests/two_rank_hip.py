@@ -39,12 +39,16 @@ def worker(rank, world, P, out):
         w, h, counts = pkg.runParallelizedSGD(data, pkg.LogisticGradient(), pkg.SquaredL2SGDUpdater(), 0.5, 4,
                                               0.01, 1.0, np.zeros(X.shape[1]), 0.001, return_chain_counts=True)
         eng_counts = np.array([c if c is not None else [] for c in counts], dtype=np.int64)
+        # tol = 0, full batches: the driver's pipelined loop (the cross-rank fold writes the host
+        # mirror of the scalars)
+        wp, hp = pkg.runParallelizedSGD(data, pkg.LogisticGradient(), pkg.SquaredL2SGDUpdater(), 0.5, 5,
+                                        0.01, 1.0, np.zeros(X.shape[1]), 0.0)
         if rank == 1:
             np.save(out + ".c1.npy", eng_counts)
         dist.barrier()
         if rank == 0:
             c1 = np.load(out + ".c1.npy")
-            np.savez(out, w=w, h=h, c0=eng_counts, c1=c1, X=X, y=y, n=X.shape[0], d=X.shape[1])
+            np.savez(out, w=w, h=h, c0=eng_counts, c1=c1, X=X, y=y, n=X.shape[0], d=X.shape[1], wp=wp, hp=hp)
     finally:
         dist.destroy_process_group()
 
