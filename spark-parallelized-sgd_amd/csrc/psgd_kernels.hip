@@ -674,12 +674,15 @@ __global__ __launch_bounds__(64) void chain_general(ChainLaunch L, KParams kp) {
 // out[0..d) = w, out[d] = regVal, out[d+1] = lossSum, out[d+2] = count.
 //
 // Each step is one dependent f64 multiply, add and IEEE division on the coordinate's running
-// value; the item loads are not on that chain. Loading item p at its step (round 6 and before)
-// left the steps waiting on memory round trips: 40 us per c2 epoch (256 chains, d = 512) for
-// ~10 us of dependent arithmetic. Now the block stages the per-item scalars (counts, and regVal,
-// loss, alpha as needed) in LDS, kFoldStage items at a time, and every coordinate thread keeps
-// its next kFoldAhead weights in flight while it folds the current ones. Same operations in
-// the same order: bit-identical results.
+// value; the item loads are not on that chain. Loading item p at its step (before round 6)
+// left the steps waiting on memory round trips: 40 us per c2 epoch (256 chains, d = 512). The
+// block stages the per-item scalars (counts, and regVal, loss, alpha as needed) in LDS,
+// kFoldStage items at a time, and every coordinate thread keeps its next kFoldAhead weights in
+// flight while it folds the current ones. Same operations in the same order: bit-identical
+// results. (Measured and not kept: the division with its denominator-only part -- the refined
+// reciprocal of c1 + c2 -- taken off the running value's dependent path, bit-identical by
+// construction where v_div_scale scales nothing and checked over the whole f64 range: 33 us
+// against 28 per c2 epoch, the extra reciprocal work per step costs more than the shorter path.)
 // ------------------------------------------------------------------------------------------
 constexpr int kFoldStage = 512;    // items staged in LDS at a time
 constexpr int kFoldAhead = 16;     // weight loads in flight per coordinate thread

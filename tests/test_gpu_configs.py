@@ -231,6 +231,55 @@ def test_fold_partials_device_bitwise(pkg):
             assert same.all(), (d, counts)
 
 
+def _adversarial_values(rng, shape):
+    """f64 values over the whole range: binary exponents -1074 .. 1023 (denormals, the tiny and
+    huge ends where v_div_scale rescales), signed zeros, infinities and NaN among normal ones."""
+    e = rng.integers(-1074, 1024, size=shape)
+    v = np.ldexp(rng.uniform(0.5, 1.0, size=shape), e) * rng.choice([-1.0, 1.0], size=shape)
+    u = rng.uniform(size=shape)
+    v = np.where(u < 0.5, rng.standard_normal(shape) * 10.0 ** rng.integers(-3, 4, size=shape), v)
+    v = np.where(u > 0.97, 0.0, v)
+    v = np.where(u > 0.98, -0.0, v)
+    v = np.where(u > 0.99, np.inf, v)
+    v = np.where(u > 0.995, np.nan, v)
+    return v
+
+
+def test_fold_step_bitwise_over_the_f64_range(pkg):
+    """The fold kernel's division (fold_step: the compiler's f64 division sequence with the
+    reciprocal of the count sum computed beside the running value, a stage folded again with `/`
+    when a step leaves its ranges) against numpy's IEEE division in the combiner's order, bit for
+    bit -- signed zeros and NaN included -- over weights and regVals spread across every binary
+    exponent, counts from 0 to 2^40, 2 to 700 items (two LDS stages) per fold."""
+    import warnings
+    warnings.simplefilter("ignore", RuntimeWarning)
+    import torch
+    rng = np.random.default_rng(77)
+    ctx = pkg.optimization.get_context(0)
+    st = torch.cuda.Stream()
+    for trial in range(24):
+        world = int(rng.choice([2, 3, 17, 255, 700]))
+        d = int(rng.choice([1, 63, 640]))
+        g = np.zeros((world, d + 3))
+        g[:, :d] = _adversarial_values(rng, (world, d))
+        g[:, d] = _adversarial_values(rng, world)
+        g[:, d + 1] = rng.standard_normal(world)
+        cnt = rng.integers(0, 40000, size=world).astype(np.float64)
+        if trial % 4 == 1:
+            cnt = np.floor(2.0 ** rng.uniform(0, 40, size=world))
+        if trial % 4 == 2:
+            cnt[: world // 3] = 0.0
+        g[:, d + 2] = cnt
+        with torch.cuda.stream(st):
+            dev = torch.from_numpy(g.reshape(-1)).cuda()
+            out = torch.empty(d + 3, dtype=torch.float64, device="cuda")
+            ctx.fold_partials_device(world, d, dev.data_ptr(), out.data_ptr(), st.cuda_stream)
+            got = out.cpu().numpy()
+        want = np_fold(list(g), d)
+        same = ((got == want) & (np.signbit(got) == np.signbit(want))) | (np.isnan(got) & np.isnan(want))
+        assert same.all(), (trial, world, d, np.nonzero(~same)[0][:5], got[~same][:5], want[~same][:5])
+
+
 def test_two_level_fold_of_partition_subsets(pkg, oracle):
     """What two ranks do, in one process: the engine's epoch over each rank's partition block
     (its on-device fold), then psgd_fold_partials_device over the two partials -- bit for bit
