@@ -3,8 +3,9 @@
 A step = one outer iteration of ParallelizedSGD.runParallelizedSGD (ParallelizedSGD.scala:237-299)
 over this GPU's partitions: the chain kernel over every partition (PSGD:243-270), the on-device
 fold (PSGD:271-276), with N > 1 the RCCL all-gather of the per-GPU partials and the cross-GPU
-fold, and the driver bookkeeping (loss, count, new weights). Inputs are synthetic and resident
-in HBM before the timed region. Default workload = BASELINE.json configs[1]
+fold, and the driver bookkeeping (loss, count, new weights) -- with tol = 0 and full batches as
+the driver's pipelined loop runs it (ParallelizedSGD._run_pipelined: epochs enqueued two ahead of
+their scalar reads). Inputs are synthetic and resident in HBM before the timed region. Default workload = BASELINE.json configs[1]
 ("Least-squares linear regression, dense 10M x 512 fp32, 256 chains on 1 MI355X"); per-GPU work
 is fixed as N grows (weak scaling: every GPU runs its own 256 chains x 10M rows).
 
