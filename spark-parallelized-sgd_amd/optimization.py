@@ -362,6 +362,10 @@ class HipEngine(ShardedEngine):
                 if time.perf_counter() - t0 > self._WAIT_LIMIT_S:
                     raise N.DeviceError("an epoch's fold did not complete")
 
+    def drain(self):
+        """Wait for everything enqueued on the engine's stream."""
+        self.stream.synchronize()
+
     def adopt_view(self, folded):
         """adopt() without the copy: the folded weights in place, intact until the second epoch
         after the one that produced them is enqueued (the result buffers alternate)."""
@@ -565,17 +569,24 @@ class ParallelizedSGD:
             log.warning("stochastic loss at step%d: %s", it, stochasticLoss)
             return avgRegVal                                       # :287
 
-        while i <= numIterations:
-            params.iteration = i
-            folded, token = engine.epoch_async(params, weights)
-            pending.append((i, token))
-            # (valid while the next epoch reads it; every later use is after its own epoch)
-            weights = engine.adopt_view(folded)                    # :286
-            if len(pending) > ParallelizedSGD.PIPELINE_LAG:
+        try:
+            while i <= numIterations:
+                params.iteration = i
+                folded, token = engine.epoch_async(params, weights)
+                pending.append((i, token))
+                # (valid while the next epoch reads it; every later use is after its own epoch)
+                weights = engine.adopt_view(folded)                # :286
+                if len(pending) > ParallelizedSGD.PIPELINE_LAG:
+                    regVal = settle(regVal)
+                i += 1
+            while pending:
                 regVal = settle(regVal)
-            i += 1
-        while pending:
-            regVal = settle(regVal)
+        except BaseException:
+            # epochs still in flight write their scalars to the engine's page-locked slots:
+            # let them finish before the error unwinds (and may free the engine)
+            if pending and hasattr(engine, "drain"):
+                engine.drain()
+            raise
         # the last epoch's weights, copied out of the alternating result buffers
         return engine.adopt(weights), regVal
 

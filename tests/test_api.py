@@ -210,3 +210,25 @@ def test_driver_pipelined_only_when_branches_are_known(pkg):
         pkg.runParallelizedSGD(data, pkg.LogisticGradient(), pkg.SimpleSGDUpdater(), 1.0, 3, 0.0, frac,
                                [0.0, 0.0], tol, engine=eng, return_chain_counts=counts)
         assert ("wait",) not in eng.log and eng.calls == 3
+
+
+def test_driver_pipelined_error_drains_inflight_epochs(pkg):
+    """An error while epochs are in flight (e.g. a watchdog NaN count read back) waits for the
+    engine's stream before it propagates: the in-flight folds write into the engine's page-locked
+    slots."""
+    data = pkg.PartitionedData.parallelize(np.ones(4), np.ones((4, 2)), 2)
+
+    class Failing(PipelinedScriptedEngine):
+        drained = False
+
+        def scalars_wait(self, token):
+            raise RuntimeError("watchdog")
+
+        def drain(self):
+            self.drained = True
+
+    eng = Failing(_scripted_results(5), 2)
+    with pytest.raises(RuntimeError, match="watchdog"):
+        pkg.runParallelizedSGD(data, pkg.LogisticGradient(), pkg.SimpleSGDUpdater(), 1.0, 5, 0.0, 1.0,
+                               [0.0, 0.0], 0.0, engine=eng)
+    assert eng.drained
