@@ -52,6 +52,29 @@ def test_pipelined_driver_matches_synchronous_loop(pkg, grad, upd, reg, compute)
     np.testing.assert_array_equal(h_p, h_s)
 
 
+@pytest.mark.parametrize("compute", ["f64", "f32"])
+def test_pipelined_driver_matches_synchronous_loop_csr(pkg, compute):
+    """CSR rows (chain_sparse_lds with an HBM tail; the fold over the chains' vectors writes the
+    mirror), Hinge + Simple and Logistic + SquaredL2: bit for bit against the synchronous loop."""
+    rng = np.random.default_rng(19)
+    n, d, P, k = 6000, 30000, 8, 24
+    rp = np.arange(n + 1, dtype=np.int64) * k
+    col = (np.sort(rng.choice(d - k, size=(n, k)), axis=1) + np.arange(k)[None, :]).astype(np.int32).reshape(-1)
+    val = rng.standard_normal(n * k)
+    if compute == "f32":
+        val = val.astype(np.float32)
+    y = (rng.uniform(size=n) > 0.5).astype(np.float64)
+    data = pkg.PartitionedData.parallelize_csr(y, rp, col, val, d, P,
+                                               dtype=np.float32 if compute == "f32" else np.float64)
+    w0 = np.zeros(d)
+    for g, u, reg in ((pkg.HingeGradient(), pkg.SimpleSGDUpdater(), 0.0),
+                      (pkg.LogisticGradient(), pkg.SquaredL2SGDUpdater(), 0.01)):
+        w_p, h_p = pkg.runParallelizedSGD(data, g, u, 0.5, 5, reg, 1.0, w0, 0.0, compute_dtype=compute)
+        w_s, h_s = _sync_loop(pkg, data, g, u, 0.5, 5, reg, w0, compute)
+        np.testing.assert_array_equal(w_p, w_s)
+        np.testing.assert_array_equal(h_p, h_s)
+
+
 def test_pipelined_driver_against_oracle(pkg, oracle):
     """fp64 at 1e-9 against the CPU restatement over enough iterations that the pipeline runs
     PIPELINE_LAG epochs ahead for most of them."""
