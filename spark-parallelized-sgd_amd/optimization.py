@@ -300,7 +300,7 @@ class HipEngine(ShardedEngine):
     # the driver's pipelined loop (ParallelizedSGD._run_pipelined) ------------------------------
     # An epoch's three scalars reach the host without a copy: the epoch's last fold kernel writes
     # them to a page-locked slot as well (psgd_run_epoch_device_mirror /
-    # psgd_fold_partials_device_mirror); the host reads the slot after the epoch's event.
+    # psgd_fold_partials_device_mirror), the count last; the host polls the count.
     _PIN_SLOTS = 16
     _mirror = None
     _mirror_next = None
@@ -542,7 +542,6 @@ class ParallelizedSGD:
         out = (engine.to_host(weights), np.array(history))
         return out + (chain_counts,) if return_chain_counts else out
 
-
     # (the number of epochs enqueued ahead of the one whose scalars are read)
     PIPELINE_LAG = 2
 
@@ -584,7 +583,7 @@ class ParallelizedSGD:
         except BaseException:
             # epochs still in flight write their scalars to the engine's page-locked slots:
             # let them finish before the error unwinds (and may free the engine)
-            if pending and hasattr(engine, "drain"):
+            if hasattr(engine, "drain"):
                 engine.drain()
             raise
         # the last epoch's weights, copied out of the alternating result buffers
