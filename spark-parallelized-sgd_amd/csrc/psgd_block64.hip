@@ -226,6 +226,10 @@ static_assert(kFixed64 % 16 == 0, "the meta and row rings start 16-byte aligned"
 #ifndef PSGD_B64_INTERLEAVE
 #define PSGD_B64_INTERLEAVE 1
 #endif
+// the next block's row reads under this block's recurrence (PREF in chain_block64; 0 for A/B)
+#ifndef PSGD_B64_PREFETCH
+#define PSGD_B64_PREFETCH 1
+#endif
 // cost probes (tools/chain_bench64 builds only; wrong results): 1 the recurrence without its
 // dependency (z not moved by the Gram terms), 2 no wait for the other chain wave's partials
 #ifndef PSGD_B64_EXP
@@ -536,19 +540,26 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
     // doubles with CONV1); rows >= kk (a tail block) are zero.
     V xraw[kB][NVH];
     double xcv[CONV1 ? kB : 1][CONV1 ? EH : 1];
-    auto load_rows = [&](auto tail_c, const char* base, int kk) __attribute__((always_inline)) {
+    // the reads of a block's rows into xraw, as stored (no use of the loaded values: a prefetch
+    // must not wait for them here)
+    auto issue_rows = [&](const char* base) __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < kB; ++k)
+#pragma unroll
+            for (int u = 0; u < NVH; ++u)
+                xraw[k][u] = *reinterpret_cast<const V*>(base + k * ROW_BYTES + (h * NVH + u) * 1024 + lane * 16);
+    };
+    // zero past the row end (stale LDS bytes) and, in a tail block, the rows >= kk; CONV1: convert
+    auto finish_rows = [&](auto tail_c, int kk) __attribute__((always_inline)) {
         constexpr bool TAIL = decltype(tail_c)::value;
 #pragma unroll
         for (int k = 0; k < kB; ++k) {
 #pragma unroll
             for (int u = 0; u < NVH; ++u) {
-                const int v = h * NVH + u;
-                V xv = *reinterpret_cast<const V*>(base + k * ROW_BYTES + v * 1024 + lane * 16);
                 if constexpr (!FULL) {
-                    if ((v * 64 + lane) * VEC >= dsc.ld) xv = V(0);
+                    if (((h * NVH + u) * 64 + lane) * VEC >= dsc.ld) xraw[k][u] = V(0);
                 }
-                if (TAIL && k >= kk) xv = V(0);
-                xraw[k][u] = xv;
+                if (TAIL && k >= kk) xraw[k][u] = V(0);
             }
         }
         if constexpr (CONV1) {
@@ -561,6 +572,14 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
                 for (int u = 0; u < NVH; ++u) unpack<S, double>(xraw[k][u], &xcv[k][u * VEC]);
         }
     };
+    // PREF (round 6): with CONV1 xraw is dead once converted, so the next block's row reads are
+    // issued into it under this block's recurrence and break test (block(); `pre` says they were)
+    // instead of at the next block's start. Measured in tools/chain_bench64 (c2 shape, f32 rows,
+    // profiles/r06_block64_prefetch_ab.log): LeastSquares with the break on 5.16 -> 4.85 ms, at
+    // tol = 0 -1 %; Logistic +8 % at c2 and, at NV = 4, 64 more live VGPRs spill (c3 +58 %) -- so
+    // only the break-on instances of the cheap multipliers at NV <= 2.
+    constexpr bool PREF = CONV1 && CONV && GRAD != G_LOGISTIC && NV <= 2 && PSGD_B64_PREFETCH;
+    bool pre = false;
     // VEC doubles of row k, slice u
     auto xrow = [&](int k, int u, double* out) __attribute__((always_inline)) {
         if constexpr (CONV1) {
@@ -736,6 +755,17 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
             const double other = xchg[((int)(b & 1) * 2 + (h ^ 1)) * kB + krow];
             z = h == 0 ? z + other : other + z;
         }
+        if constexpr (PREF && !TAIL) {
+            // the next full block's rows, if they have landed (the count read at this block's
+            // start), into xraw: their LDS round trip runs under the recurrence and the test.
+            // After the exchange's read (LDS returns in order: issued earlier, they would delay
+            // it); the memory clobber keeps the compiler from hoisting them above it or above
+            // the count they follow (LDS executes one wave's operations in order)
+            asm volatile("" : "+v"(z) : : "memory");
+            const unsigned rr = rpre > ready ? rpre : ready;
+            pre = b + 1 < nfull && (int64_t)rr >= (b + 2) * kB;
+            if (pre) issue_rows(ring + (rs + kB == R ? 0 : rs + kB) * ROW_BYTES);
+        }
         PSGD_STAMP(const uint64_t st_xe = __builtin_amdgcn_s_memtime(); st_x += st_xe - st_g;)
 
         // the scalar recurrence: c_i from z_i, then every later row's dot moves by c_i G[k][i]
@@ -856,15 +886,19 @@ void chain_block64(ChainLaunch L, KParams kp, RingGeom geom) {
     using Tail = std::integral_constant<bool, true>;
     bool ok = true;
     for (int64_t b = 0; ok && !conv_stop && b < nfull; ++b) {
-        PSGD_STAMP(const uint64_t st_w = __builtin_amdgcn_s_memtime();)
-        ok = wait_rows((b + 1) * kB);
-        PSGD_STAMP(st_rd += __builtin_amdgcn_s_memtime() - st_w;)
-        if (!ok) break;
-        load_rows(Full{}, ring + rs * ROW_BYTES, kB);
+        if (!pre) {   // (PREF: the previous block issued these reads)
+            PSGD_STAMP(const uint64_t st_w = __builtin_amdgcn_s_memtime();)
+            ok = wait_rows((b + 1) * kB);
+            PSGD_STAMP(st_rd += __builtin_amdgcn_s_memtime() - st_w;)
+            if (!ok) break;
+            issue_rows(ring + rs * ROW_BYTES);
+        }
+        finish_rows(Full{}, kB);
         ok = block(Full{}, b, kB);
     }
     if (ok && !conv_stop && ntail > 0 && wait_rows(n)) {
-        load_rows(Tail{}, ring + rs * ROW_BYTES, ntail);
+        issue_rows(ring + rs * ROW_BYTES);
+        finish_rows(Tail{}, ntail);
         block(Tail{}, nfull, ntail);
     }
     // a wave that stopped early leaves the others blocked on it: wake them
